@@ -1,0 +1,450 @@
+// fs_api.cpp -- host side of libfootsies.so: the extern "C" entry points of
+// include/footsies.h over the HIP kernels in fs_kernels.hip.
+//
+// One handle owns one device, one non-blocking HIP stream, the arena state in
+// HBM and the output buffers.  Nothing here touches the simulation semantics;
+// see fs_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "fs_internal.h"
+
+#define FS_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Buffers {
+  // outputs (library-owned)
+  uint8_t *guard = nullptr, *move = nullptr, *action = nullptr, *hitstun = nullptr, *terminated = nullptr,
+          *truncated = nullptr;
+  float *move_frame = nullptr, *position = nullptr;
+  double* reward = nullptr;
+  int32_t* frame = nullptr;
+  uint8_t *f_guard = nullptr, *f_move = nullptr, *f_action = nullptr, *f_hitstun = nullptr;
+  float *f_move_frame = nullptr, *f_position = nullptr;
+  int32_t* f_frame = nullptr;
+};
+
+}  // namespace
+
+struct fs_context {
+  fs_config cfg{};
+  int n = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;      // the stream all work is issued on
+  hipStream_t own_stream = nullptr;  // the library's own stream
+  fsk::DevState st{};
+  Buffers own{};
+  fsk::DevOutputs out{};  // what the kernels write (own buffers or caller-bound ones)
+  // staging for host-side actions / reset arguments
+  uint8_t* d_act = nullptr;      // [2][N]
+  uint8_t* h_act = nullptr;      // pinned [2][N]
+  uint64_t* d_seeds = nullptr;   // [N]
+  uint64_t* h_seeds = nullptr;   // pinned [N]
+  uint8_t* d_mask = nullptr;     // [N]
+  uint8_t* h_mask = nullptr;     // pinned [N]
+  hipEvent_t staging_free = nullptr;
+  std::vector<void*> allocations;
+  uint64_t steps = 0;
+  std::string err;
+};
+
+namespace {
+
+int set_err(fs_context* h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf;
+  else g_create_error = buf;
+  return code;
+}
+
+#define HIP_TRY(h, expr)                                                                              \
+  do {                                                                                                \
+    hipError_t e_ = (expr);                                                                           \
+    if (e_ != hipSuccess) return set_err((h), FS_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+template <typename T>
+int dalloc(fs_context* h, T** p, size_t count) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, count * sizeof(T) ? count * sizeof(T) : 1);
+  if (e != hipSuccess) return set_err(h, FS_E_OOM, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+  h->allocations.push_back(q);
+  *p = static_cast<T*>(q);
+  return FS_OK;
+}
+
+void free_all(fs_context* h) {
+  for (void* p : h->allocations) (void)hipFree(p);
+  h->allocations.clear();
+  if (h->h_act) (void)hipHostFree(h->h_act);
+  if (h->h_seeds) (void)hipHostFree(h->h_seeds);
+  if (h->h_mask) (void)hipHostFree(h->h_mask);
+  if (h->staging_free) (void)hipEventDestroy(h->staging_free);
+  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+  h->own_stream = nullptr;
+  h->h_act = nullptr;
+  h->h_seeds = nullptr;
+  h->h_mask = nullptr;
+  h->staging_free = nullptr;
+  h->stream = nullptr;
+}
+
+int use_device(fs_context* h) {
+  HIP_TRY(h, hipSetDevice(h->device));
+  return FS_OK;
+}
+
+void outputs_from_own(fs_context* h) {
+  Buffers& b = h->own;
+  h->out = fsk::DevOutputs{b.guard,   b.move,   b.move_frame, b.position,     b.reward,     b.terminated,
+                           b.truncated, b.frame, b.action,    b.hitstun,      b.f_guard,    b.f_move,
+                           b.f_move_frame, b.f_position, b.f_frame, b.f_action, b.f_hitstun};
+}
+
+// wait until the pinned staging buffers may be overwritten
+int staging_wait(fs_context* h) {
+  HIP_TRY(h, hipEventSynchronize(h->staging_free));
+  return FS_OK;
+}
+
+}  // namespace
+
+FS_API int fs_abi_version(void) { return FS_ABI_VERSION; }
+
+FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
+  g_create_error.clear();
+  if (!cfg || !out) return set_err(nullptr, FS_E_INVALID, "fs_create: null argument");
+  *out = nullptr;
+  if (cfg->num_envs <= 0) return set_err(nullptr, FS_E_INVALID, "num_envs must be > 0 (got %d)", cfg->num_envs);
+  if (cfg->p2_mode < FS_P2_EXTERNAL || cfg->p2_mode > FS_P2_NOOP)
+    return set_err(nullptr, FS_E_INVALID, "invalid p2_mode %d", cfg->p2_mode);
+  if (cfg->float_mode != FS_FLOAT_STRICT32 && cfg->float_mode != FS_FLOAT_DOUBLE)
+    return set_err(nullptr, FS_E_INVALID, "invalid float_mode %d", cfg->float_mode);
+  if (cfg->autoreset_mode != FS_AUTORESET_SAME_STEP && cfg->autoreset_mode != FS_AUTORESET_NEXT_STEP)
+    return set_err(nullptr, FS_E_INVALID, "invalid autoreset_mode %d", cfg->autoreset_mode);
+  if (cfg->frame_delay != 0)
+    return set_err(nullptr, FS_E_UNSUPPORTED, "frame_delay=%d is not supported (only 0)", cfg->frame_delay);
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0)
+    return set_err(nullptr, FS_E_DEVICE, "no HIP device available (%s)", hipGetErrorString(e));
+  if (cfg->device_id < 0 || cfg->device_id >= ndev)
+    return set_err(nullptr, FS_E_INVALID, "device_id %d out of range (%d devices)", cfg->device_id, ndev);
+
+  fs_context* h = new (std::nothrow) fs_context();
+  if (!h) return set_err(nullptr, FS_E_OOM, "out of host memory");
+  h->cfg = *cfg;
+  h->n = cfg->num_envs;
+  h->device = cfg->device_id;
+  const size_t N = (size_t)h->n;
+  const bool bot = cfg->p2_mode == FS_P2_BOT;
+  int rc = FS_OK;
+  auto fail = [&](int code) {
+    std::string msg = h->err;
+    free_all(h);
+    delete h;
+    g_create_error = msg;
+    return code;
+  };
+  if ((rc = use_device(h)) != FS_OK) return fail(rc);
+  if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_err(h, FS_E_DEVICE, "hipStreamCreate failed"));
+  h->stream = h->own_stream;
+  if (hipEventCreateWithFlags(&h->staging_free, hipEventDisableTiming) != hipSuccess)
+    return fail(set_err(h, FS_E_DEVICE, "hipEventCreate failed"));
+  // state
+  if ((rc = dalloc(h, &h->st.pos, N)) || (rc = dalloc(h, &h->st.hist, N)) || (rc = dalloc(h, &h->st.fpk, N)) ||
+      (rc = dalloc(h, &h->st.aw, N)) || (rc = dalloc(h, &h->st.cum, N)))
+    return fail(rc);
+  if (bot && ((rc = dalloc(h, &h->st.rng, N)) || (rc = dalloc(h, &h->st.bot, N)))) return fail(rc);
+  // outputs
+  Buffers& b = h->own;
+  if ((rc = dalloc(h, &b.guard, 2 * N)) || (rc = dalloc(h, &b.move, 2 * N)) || (rc = dalloc(h, &b.action, 2 * N)) ||
+      (rc = dalloc(h, &b.hitstun, 2 * N)) || (rc = dalloc(h, &b.terminated, N)) || (rc = dalloc(h, &b.truncated, N)) ||
+      (rc = dalloc(h, &b.move_frame, 2 * N)) || (rc = dalloc(h, &b.position, 2 * N)) ||
+      (rc = dalloc(h, &b.reward, N)) || (rc = dalloc(h, &b.frame, N)) || (rc = dalloc(h, &b.f_guard, 2 * N)) ||
+      (rc = dalloc(h, &b.f_move, 2 * N)) || (rc = dalloc(h, &b.f_action, 2 * N)) ||
+      (rc = dalloc(h, &b.f_hitstun, 2 * N)) || (rc = dalloc(h, &b.f_move_frame, 2 * N)) ||
+      (rc = dalloc(h, &b.f_position, 2 * N)) || (rc = dalloc(h, &b.f_frame, N)))
+    return fail(rc);
+  // staging
+  if ((rc = dalloc(h, &h->d_act, 2 * N)) || (rc = dalloc(h, &h->d_seeds, N)) || (rc = dalloc(h, &h->d_mask, N)))
+    return fail(rc);
+  if (hipHostMalloc((void**)&h->h_act, 2 * N, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&h->h_seeds, N * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&h->h_mask, N, hipHostMallocDefault) != hipSuccess)
+    return fail(set_err(h, FS_E_OOM, "hipHostMalloc failed"));
+  outputs_from_own(h);
+  // zero the final_* rows so untouched rows read deterministically
+  for (void* p : {(void*)b.f_guard, (void*)b.f_move, (void*)b.f_action, (void*)b.f_hitstun})
+    if (hipMemsetAsync(p, 0, 2 * N, h->stream) != hipSuccess) return fail(set_err(h, FS_E_DEVICE, "memset"));
+  if (hipMemsetAsync(b.f_move_frame, 0, 2 * N * sizeof(float), h->stream) != hipSuccess ||
+      hipMemsetAsync(b.f_position, 0, 2 * N * sizeof(float), h->stream) != hipSuccess ||
+      hipMemsetAsync(b.f_frame, 0, N * sizeof(int32_t), h->stream) != hipSuccess)
+    return fail(set_err(h, FS_E_DEVICE, "memset"));
+  if (hipEventRecord(h->staging_free, h->stream) != hipSuccess) return fail(set_err(h, FS_E_DEVICE, "event"));
+  // game start: Stop -> Intro -> Fight (state(-1))
+  fsk::ResetParams rp{};
+  rp.st = h->st;
+  rp.out = h->out;
+  rp.n_envs = h->n;
+  rp.flags = FS_RESET_HARD;
+  rp.init = 1;
+  rp.base_seed = cfg->base_seed;
+  hipError_t le = fsk::launch_reset(rp, cfg->float_mode, cfg->p2_mode, h->stream);
+  if (le != hipSuccess) return fail(set_err(h, FS_E_DEVICE, "reset kernel launch: %s", hipGetErrorString(le)));
+  le = hipStreamSynchronize(h->stream);
+  if (le != hipSuccess) return fail(set_err(h, FS_E_DEVICE, "reset kernel: %s", hipGetErrorString(le)));
+  *out = h;
+  return FS_OK;
+}
+
+FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int flags) {
+  if (!h) return FS_E_INVALID;
+  if (flags != FS_RESET_HARD && flags != FS_RESET_IF_NEEDED) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  if ((rc = staging_wait(h))) return rc;
+  const size_t N = (size_t)h->n;
+  fsk::ResetParams rp{};
+  rp.st = h->st;
+  rp.out = h->out;
+  rp.n_envs = h->n;
+  rp.flags = flags;
+  rp.init = 0;
+  if (seeds) {
+    memcpy(h->h_seeds, seeds, N * sizeof(uint64_t));
+    HIP_TRY(h, hipMemcpyAsync(h->d_seeds, h->h_seeds, N * sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
+    rp.seeds = h->d_seeds;
+  }
+  if (mask) {
+    memcpy(h->h_mask, mask, N);
+    HIP_TRY(h, hipMemcpyAsync(h->d_mask, h->h_mask, N, hipMemcpyHostToDevice, h->stream));
+    rp.mask = h->d_mask;
+  }
+  HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
+  HIP_TRY(h, fsk::launch_reset(rp, h->cfg.float_mode, h->cfg.p2_mode, h->stream));
+  return FS_OK;
+}
+
+static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2, int flags, uint64_t seed,
+                       const fs_outputs* traj) {
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  const size_t N = (size_t)h->n;
+  fsk::StepParams sp{};
+  sp.st = h->st;
+  sp.out = h->out;
+  sp.n_envs = h->n;
+  sp.n_steps = n;
+  sp.out_stride_steps = 0;
+  sp.dense_reward = h->cfg.dense_reward;
+  sp.autoreset_mode = h->cfg.autoreset_mode;
+  sp.action_seed = seed;
+  sp.t0 = h->steps;
+  const bool ext = h->cfg.p2_mode == FS_P2_EXTERNAL;
+  if (flags == FS_ACT_HOST && p1) {
+    if (n != 1) return set_err(h, FS_E_INVALID, "host actions are only accepted for single steps");
+    if ((rc = staging_wait(h))) return rc;
+    memcpy(h->h_act, p1, N);
+    if (ext) memcpy(h->h_act + N, p2, N);
+    HIP_TRY(h, hipMemcpyAsync(h->d_act, h->h_act, ext ? 2 * N : N, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
+    sp.p1 = h->d_act;
+    sp.p2 = ext ? h->d_act + N : nullptr;
+  } else {
+    sp.p1 = p1;
+    sp.p2 = ext ? p2 : nullptr;
+  }
+  if (traj) {
+    sp.out = fsk::DevOutputs{traj->guard,          traj->move,           traj->move_frame,  traj->position,
+                             traj->reward,         traj->terminated,     traj->truncated,   traj->frame,
+                             traj->action,         traj->hitstun,        traj->final_guard, traj->final_move,
+                             traj->final_move_frame, traj->final_position, traj->final_frame, traj->final_action,
+                             traj->final_hitstun};
+    const void* req[] = {traj->guard, traj->move,   traj->move_frame, traj->position, traj->reward,
+                         traj->terminated, traj->truncated, traj->frame, traj->action, traj->hitstun};
+    for (const void* q : req)
+      if (!q) return set_err(h, FS_E_INVALID, "fs_step_n: trajectory buffer missing");
+    if (h->cfg.autoreset_mode == FS_AUTORESET_SAME_STEP &&
+        (!traj->final_guard || !traj->final_move || !traj->final_move_frame || !traj->final_position ||
+         !traj->final_frame || !traj->final_action || !traj->final_hitstun))
+      return set_err(h, FS_E_INVALID, "fs_step_n: final_* trajectory buffers required in same-step autoreset");
+    sp.out_stride_steps = 1;
+  }
+  HIP_TRY(h, fsk::launch_step(sp, h->cfg.float_mode, h->cfg.p2_mode, h->stream));
+  h->steps += (uint64_t)n;
+  return FS_OK;
+}
+
+FS_API int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags) {
+  if (!h) return FS_E_INVALID;
+  if (!p1_act) return set_err(h, FS_E_INVALID, "fs_step: p1 actions required");
+  if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
+    return set_err(h, FS_E_INVALID, "fs_step: p2 actions required for FS_P2_EXTERNAL");
+  if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
+  return step_common(h, 1, p1_act, p2_act, flags, 0, nullptr);
+}
+
+FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act, uint64_t action_seed,
+                     const fs_outputs* traj) {
+  if (!h) return FS_E_INVALID;
+  if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n: n must be > 0");
+  if ((p1_act == nullptr) != (p2_act == nullptr) && h->cfg.p2_mode == FS_P2_EXTERNAL)
+    return set_err(h, FS_E_INVALID, "fs_step_n: give both action arrays or neither");
+  return step_common(h, n, p1_act, p2_act, FS_ACT_DEVICE, action_seed, traj);
+}
+
+FS_API int fs_outputs_get(fs_handle h, fs_outputs* o) {
+  if (!h || !o) return FS_E_INVALID;
+  const fsk::DevOutputs& d = h->out;
+  *o = fs_outputs{d.guard,        d.move,           d.move_frame,  d.position,     d.reward,       d.terminated,
+                  d.truncated,    d.frame,          d.action,      d.hitstun,      d.final_guard,  d.final_move,
+                  d.final_move_frame, d.final_position, d.final_frame, d.final_action, d.final_hitstun};
+  return FS_OK;
+}
+
+FS_API int fs_bind_outputs(fs_handle h, const fs_outputs* dev) {
+  if (!h) return FS_E_INVALID;
+  outputs_from_own(h);
+  if (!dev) return FS_OK;
+#define BIND(f, g) \
+  if (dev->f) h->out.g = dev->f
+  BIND(guard, guard);
+  BIND(move, move);
+  BIND(move_frame, move_frame);
+  BIND(position, position);
+  BIND(reward, reward);
+  BIND(terminated, terminated);
+  BIND(truncated, truncated);
+  BIND(frame, frame);
+  BIND(action, action);
+  BIND(hitstun, hitstun);
+  BIND(final_guard, final_guard);
+  BIND(final_move, final_move);
+  BIND(final_move_frame, final_move_frame);
+  BIND(final_position, final_position);
+  BIND(final_frame, final_frame);
+  BIND(final_action, final_action);
+  BIND(final_hitstun, final_hitstun);
+#undef BIND
+  return FS_OK;
+}
+
+FS_API int fs_get_env_state(fs_handle h, fs_env_state* host_out) {
+  if (!h || !host_out) return FS_E_INVALID;
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  fs_env_state* d = nullptr;
+  HIP_TRY(h, hipMalloc(&d, sizeof(fs_env_state) * (size_t)h->n));
+  hipError_t e = fsk::launch_get_state(h->st, nullptr, d, h->n, h->cfg.p2_mode, h->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(host_out, d, sizeof(fs_env_state) * (size_t)h->n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return set_err(h, FS_E_DEVICE, "fs_get_env_state: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
+FS_API int fs_get_state(fs_handle h, fs_arena_state* host_out) {
+  if (!h || !host_out) return FS_E_INVALID;
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  fs_arena_state* d = nullptr;
+  HIP_TRY(h, hipMalloc(&d, sizeof(fs_arena_state) * (size_t)h->n));
+  hipError_t e = fsk::launch_get_state(h->st, d, nullptr, h->n, h->cfg.p2_mode, h->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(host_out, d, sizeof(fs_arena_state) * (size_t)h->n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return set_err(h, FS_E_DEVICE, "fs_get_state: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
+static const int32_t kIds[] = {0, 1, 2, 10, 11, 100, 105, 110, 115, 200, 301, 305, 306, 310, 350, 500, 510};
+static bool valid_action_id(int32_t id) {
+  for (int32_t k : kIds)
+    if (k == id) return true;
+  return false;
+}
+
+FS_API int fs_set_state(fs_handle h, const fs_arena_state* host_in) {
+  if (!h || !host_in) return FS_E_INVALID;
+  for (int i = 0; i < h->n; i++) {  // the packed layout's ranges (fs_kernels.hip)
+    const fs_arena_state& s = host_in[i];
+    for (int k = 0; k < 2; k++) {
+      const fs_fighter_state& f = s.f[k];
+      if (!valid_action_id(f.action_id) || f.action_frame < 0 || f.action_frame > 511 || f.hitstun < 0 ||
+          f.hitstun > 31 || f.vital < 0 || f.vital > 3 || f.guard < 0 || f.guard > 3 || f.hit_count < 0 ||
+          f.hit_count > 3 || f.attack_hold < 0 || f.attack_hold > 63 ||
+          (f.buffer_action_id != -1 && !valid_action_id(f.buffer_action_id)) ||
+          (f.reserve_action_id != -1 && !valid_action_id(f.reserve_action_id)))
+        return set_err(h, FS_E_INVALID, "fs_set_state: arena %d fighter %d out of representable range", i, k);
+    }
+    if (s.recording_count < 0 || s.recording_count > 18000)
+      return set_err(h, FS_E_INVALID, "fs_set_state: arena %d recording_count out of range", i);
+    if (h->cfg.p2_mode == FS_P2_BOT &&
+        (s.move_plan < -1 || s.move_plan > 6 || s.attack_plan < -1 || s.attack_plan > 4 || s.move_index < 0 ||
+         s.move_index > 127 || s.attack_index < 0 || s.attack_index > 127 ||
+         !valid_action_id(s.prev_opponent_action)))
+      return set_err(h, FS_E_INVALID, "fs_set_state: arena %d bot state out of range", i);
+  }
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  fs_arena_state* d = nullptr;
+  HIP_TRY(h, hipMalloc(&d, sizeof(fs_arena_state) * (size_t)h->n));
+  hipError_t e = hipMemcpyAsync(d, host_in, sizeof(fs_arena_state) * (size_t)h->n, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = fsk::launch_set_state(h->st, d, h->n, h->cfg.p2_mode, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return set_err(h, FS_E_DEVICE, "fs_set_state: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
+FS_API int fs_sync(fs_handle h) {
+  if (!h) return FS_E_INVALID;
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return FS_OK;
+}
+
+FS_API void* fs_stream(fs_handle h) { return h ? (void*)h->stream : nullptr; }
+FS_API int fs_set_stream(fs_handle h, void* stream) {
+  if (!h) return FS_E_INVALID;
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  hipStream_t next = stream == FS_STREAM_OWN ? h->own_stream : (hipStream_t)stream;
+  if (next == h->stream) return FS_OK;
+  // order the new stream after everything already issued on the old one
+  HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
+  HIP_TRY(h, hipStreamWaitEvent(next, h->staging_free, 0));
+  h->stream = next;
+  HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
+  return FS_OK;
+}
+
+FS_API int fs_num_envs(fs_handle h) { return h ? h->n : 0; }
+FS_API uint64_t fs_steps_taken(fs_handle h) { return h ? h->steps : 0; }
+
+FS_API void fs_destroy(fs_handle h) {
+  if (!h) return;
+  if (hipSetDevice(h->device) == hipSuccess && h->stream) (void)hipStreamSynchronize(h->stream);
+  free_all(h);
+  delete h;
+}
+
+FS_API const char* fs_last_error(fs_handle h) { return h ? h->err.c_str() : g_create_error.c_str(); }

@@ -1,0 +1,246 @@
+"""FootsiesSim: a thin, zero-copy handle over libfootsies.so for N arenas on one GPU.
+
+PyTorch is used only as device-memory and stream plumbing: the output buffers are
+torch tensors bound into the library (``fs_bind_outputs``) and the library runs
+on torch's current stream (``fs_set_stream``), so device-side actions produced
+by a policy and the observations consumed by it need no extra synchronisation.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._lib import check, lib
+
+P2_MODES = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT, "noop": _abi.FS_P2_NOOP}
+FLOAT_MODES = {"strict": _abi.FS_FLOAT_STRICT32, "double": _abi.FS_FLOAT_DOUBLE}
+AUTORESET_MODES = {"same_step": _abi.FS_AUTORESET_SAME_STEP, "next_step": _abi.FS_AUTORESET_NEXT_STEP}
+
+_TORCH_DTYPES = {"u1": "uint8", "f4": "float32", "f8": "float64", "i4": "int32"}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def encode_actions(actions):
+    """(N,3) booleans (left, right, attack) or (N,) ints 0..7 -> uint8 3-bit inputs.
+
+    Mirrors TrainingRemoteActor.RequestTrainingInput (TrainingRemoteActor.cs:112-116):
+    byte 0 -> Left(1), byte 1 -> Right(2), byte 2 -> Attack(4), non-zero = pressed.
+    """
+    a = np.asarray(actions)
+    if a.ndim == 2:
+        if a.shape[1] != 3:
+            raise ValueError("actions must be (N,3) booleans or (N,) ints, got shape %s" % (a.shape,))
+        a = a != 0
+        return (a[:, 0].astype(np.uint8) | (a[:, 1].astype(np.uint8) << 1) | (a[:, 2].astype(np.uint8) << 2))
+    if a.ndim == 1:
+        if a.size and (a.min() < 0 or a.max() > 7):
+            raise ValueError("integer actions must be in 0..7")
+        return a.astype(np.uint8)
+    raise ValueError("actions must be (N,3) booleans or (N,) ints, got shape %s" % (a.shape,))
+
+
+def decode_actions(bits):
+    """uint8 3-bit inputs -> (N,3) booleans (FootsiesState.__post_init__, state.py:26-36)."""
+    b = np.asarray(bits, dtype=np.uint8)
+    return np.stack([(b & 1) != 0, (b & 2) != 0, (b & 4) != 0], axis=-1)
+
+
+class FootsiesSim:
+    """N independent FOOTSIES arenas on one MI355X.
+
+    Parameters mirror ``fs_config`` (include/footsies.h).  ``outputs()`` returns
+    torch tensors on the device that are overwritten by the next call.
+    """
+
+    def __init__(self, num_envs, device=0, p2_mode="bot", dense_reward=True, float_mode="strict",
+                 autoreset_mode="same_step", seed=0, frame_delay=0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError("FootsiesSim needs a HIP device (torch.cuda.is_available() is False)")
+        if p2_mode not in P2_MODES:
+            raise ValueError("p2_mode must be one of %s" % list(P2_MODES))
+        if float_mode not in FLOAT_MODES:
+            raise ValueError("float_mode must be one of %s" % list(FLOAT_MODES))
+        if autoreset_mode not in AUTORESET_MODES:
+            raise ValueError("autoreset_mode must be one of %s" % list(AUTORESET_MODES))
+        self.num_envs = int(num_envs)
+        self.device = torch.device("cuda", device)
+        self.p2_mode = p2_mode
+        self.autoreset_mode = autoreset_mode
+        cfg = _abi.fs_config(num_envs=self.num_envs, device_id=device, p2_mode=P2_MODES[p2_mode],
+                             dense_reward=int(bool(dense_reward)), frame_delay=int(frame_delay),
+                             float_mode=FLOAT_MODES[float_mode], autoreset_mode=AUTORESET_MODES[autoreset_mode],
+                             base_seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
+        h = C.c_void_p()
+        check(lib().fs_create(C.byref(cfg), C.byref(h)), None)
+        self._h = h
+        self.cfg = cfg
+        # outputs: torch tensors bound into the library
+        n = self.num_envs
+        self._out = {}
+        with torch.cuda.device(self.device):
+            for name, (dt, cols) in _abi.OUTPUT_SPEC.items():
+                shape = (n, cols) if cols > 1 else (n,)
+                self._out[name] = torch.zeros(shape, dtype=getattr(torch, _TORCH_DTYPES[dt]), device=self.device)
+        # the library's creation-time outputs (state(-1)) into the bound buffers
+        own = _abi.fs_outputs()
+        check(lib().fs_outputs_get(h, C.byref(own)), h)
+        check(lib().fs_sync(h), h)
+        for name in _abi.OUTPUT_SPEC:
+            t = self._out[name]
+            _copy_device(t.data_ptr(), getattr(own, name), t.numel() * t.element_size())
+        bind = _abi.fs_outputs(**{name: t.data_ptr() for name, t in self._out.items()})
+        check(lib().fs_bind_outputs(h, C.byref(bind)), h)
+        self.use_torch_stream()
+
+    # -- streams ---------------------------------------------------------------------
+    def use_torch_stream(self, stream=None):
+        """Issue all further work on ``stream`` (default: torch's current stream)."""
+        torch = _torch()
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        check(lib().fs_set_stream(self._h, C.c_void_p(s.cuda_stream)), self._h)
+
+    # -- core API --------------------------------------------------------------------
+    def reset(self, seeds=None, mask=None, hard=False):
+        """FootsiesEnv.reset over all (or the masked) arenas; seeds -> Random.InitState."""
+        n = self.num_envs
+        s = None if seeds is None else np.ascontiguousarray(np.broadcast_to(np.asarray(seeds, dtype=np.uint64), (n,)))
+        m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(n))
+        flags = _abi.FS_RESET_HARD if hard else _abi.FS_RESET_IF_NEEDED
+        check(lib().fs_reset(self._h, None if s is None else s.ctypes.data, None if m is None else m.ctypes.data,
+                             flags), self._h)
+        return self._out
+
+    def step(self, p1, p2=None):
+        """One env-step of every arena.  Actions: torch uint8 device tensors [N] (fast path) or
+        host arrays ((N,3) bools or (N,) ints)."""
+        torch = _torch()
+        ext = self.p2_mode == "external"
+        if ext and p2 is None:
+            raise ValueError("p2 actions are required when p2_mode='external'")
+        if isinstance(p1, torch.Tensor) and p1.is_cuda:
+            p1 = _as_u8_device(p1, self.num_envs)
+            p2t = _as_u8_device(p2, self.num_envs) if ext else None
+            check(lib().fs_step(self._h, C.c_void_p(p1.data_ptr()),
+                                C.c_void_p(p2t.data_ptr()) if ext else None, _abi.FS_ACT_DEVICE), self._h)
+        else:
+            a1 = np.ascontiguousarray(encode_actions(_host(p1)))
+            a2 = np.ascontiguousarray(encode_actions(_host(p2))) if ext else None
+            if a1.shape[0] != self.num_envs or (a2 is not None and a2.shape[0] != self.num_envs):
+                raise ValueError("expected %d actions" % self.num_envs)
+            check(lib().fs_step(self._h, a1.ctypes.data, None if a2 is None else a2.ctypes.data,
+                                _abi.FS_ACT_HOST), self._h)
+        return self._out
+
+    def step_n(self, n, p1=None, p2=None, action_seed=0, trajectory=None):
+        """n ticks in one kernel launch.  p1/p2: device uint8 [n][N] or None (on-device hashed
+        actions).  trajectory: dict of device tensors shaped [n][N](,2) like ``alloc_trajectory``."""
+        t = None
+        if trajectory is not None:
+            t = _abi.fs_outputs(**{k: trajectory[k].data_ptr() for k in _abi.OUTPUT_SPEC if k in trajectory})
+        check(lib().fs_step_n(self._h, int(n), None if p1 is None else C.c_void_p(p1.data_ptr()),
+                              None if p2 is None else C.c_void_p(p2.data_ptr()), int(action_seed) & (2**64 - 1),
+                              None if t is None else C.byref(t)), self._h)
+        return trajectory if trajectory is not None else self._out
+
+    def alloc_trajectory(self, n):
+        torch = _torch()
+        out = {}
+        for name, (dt, cols) in _abi.OUTPUT_SPEC.items():
+            shape = (n, self.num_envs, cols) if cols > 1 else (n, self.num_envs)
+            out[name] = torch.zeros(shape, dtype=getattr(torch, _TORCH_DTYPES[dt]), device=self.device)
+        return out
+
+    def outputs(self):
+        return self._out
+
+    def outputs_numpy(self):
+        _torch().cuda.synchronize(self.device)
+        return {k: v.cpu().numpy() for k, v in self._out.items()}
+
+    def env_state(self):
+        arr = (_abi.fs_env_state * self.num_envs)()
+        check(lib().fs_get_env_state(self._h, arr), self._h)
+        return np.ctypeslib.as_array(arr).copy()
+
+    def get_state(self):
+        arr = (_abi.fs_arena_state * self.num_envs)()
+        check(lib().fs_get_state(self._h, arr), self._h)
+        return np.ctypeslib.as_array(arr).copy()
+
+    def set_state(self, state):
+        state = np.ascontiguousarray(state)
+        if state.shape != (self.num_envs,):
+            raise ValueError("state must have shape (%d,)" % self.num_envs)
+        arr = (_abi.fs_arena_state * self.num_envs).from_buffer_copy(state.tobytes())
+        check(lib().fs_set_state(self._h, arr), self._h)
+
+    def sync(self):
+        check(lib().fs_sync(self._h), self._h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def steps_taken(self):
+        return int(lib().fs_steps_taken(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().fs_sync(self._h)
+            lib().fs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _host(a):
+    torch = _torch()
+    if isinstance(a, torch.Tensor):
+        return a.detach().cpu().numpy()
+    return a
+
+
+def _as_u8_device(t, n):
+    torch = _torch()
+    if t.dim() == 2 and t.shape[1] == 3:
+        t = t.to(torch.uint8)
+        t = t[:, 0] | (t[:, 1] << 1) | (t[:, 2] << 2)
+    if t.dtype != torch.uint8:
+        t = t.to(torch.uint8)
+    t = t.contiguous()
+    if t.shape != (n,):
+        raise ValueError("expected device actions of shape (%d,), got %s" % (n, tuple(t.shape)))
+    return t
+
+
+_hip = None
+
+
+def _copy_device(dst, src, nbytes):
+    """hipMemcpy device->device through the HIP runtime (used once at construction)."""
+    global _hip
+    if _hip is None:
+        import ctypes.util
+        for name in ("libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"):
+            try:
+                _hip = C.CDLL(name)
+                break
+            except OSError:
+                continue
+        if _hip is None:
+            raise RuntimeError("libamdhip64 not found")
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipMemcpy.restype = C.c_int
+    rc = _hip.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, 3)  # hipMemcpyDeviceToDevice
+    if rc != 0:
+        raise RuntimeError("hipMemcpy failed: %d" % rc)

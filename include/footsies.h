@@ -1,0 +1,232 @@
+/*
+ * footsies.h -- C-ABI of libfootsies.so, the MI355X-native vectorized FOOTSIES
+ * simulator (HIP kernels for gfx950).
+ *
+ * The reference has no native FFI for this path: its boundary is a Python
+ * gymnasium.Env (FootsiesEnv) talking over TCP to a Unity process.  Every entry
+ * point below replaces one piece of that stack for N independent arenas at once;
+ * the piece is cited next to it (paths relative to the reference root,
+ * FE = footsies-gym/footsies_gym/envs/footsies.py, BC = Assets/Script/BattleCore.cs).
+ *
+ * Conventions
+ *   - plain C types only; no exceptions cross the ABI; every call returns 0 on
+ *     success or a negative FS_E_* code, with a message via fs_last_error();
+ *   - one handle = one device + one HIP stream; calls on a handle must be
+ *     serialised by the caller, different handles may run on different threads;
+ *   - the library allocates and owns its device buffers; caller buffers are
+ *     borrowed for the duration of the call only (unless bound with
+ *     fs_bind_outputs, see below);
+ *   - fs_step / fs_step_n / fs_reset are asynchronous on the handle's stream;
+ *     fs_sync() or the caller's own stream sync orders host reads.
+ */
+#ifndef FOOTSIES_H
+#define FOOTSIES_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FS_ABI_VERSION 1
+
+/* error codes */
+#define FS_OK 0
+#define FS_E_INVALID (-1)      /* bad argument (FE:100-108 raises ValueError for bad ctor args) */
+#define FS_E_DEVICE (-2)       /* HIP runtime failure / no device */
+#define FS_E_UNSUPPORTED (-3)  /* configuration not implemented (e.g. frame_delay > 0) */
+#define FS_E_OOM (-4)
+
+/* P2 controller (GameManager.cs:183-190: --p2-bot / remote actor; FE:234-247) */
+#define FS_P2_EXTERNAL 0  /* P2 action supplied every step (FE `opponent` callable / remote actor) */
+#define FS_P2_BOT 1       /* the in-game scripted BattleAI (BattleAI.cs:10-403) as TrainingBattleAIActor */
+#define FS_P2_NOOP 2      /* P2 input always 0 */
+
+/* Float evaluation model of the C# arithmetic (parity-unpinned: no Unity binary here) */
+#define FS_FLOAT_STRICT32 0  /* every float expression rounded to IEEE binary32 per operation (default) */
+#define FS_FLOAT_DOUBLE 1    /* expression temporaries in binary64, rounded to binary32 on store/call */
+
+/* Auto-reset of terminated arenas inside fs_step (the Unity KO->End->Stop->Intro->Fight
+ * burst, BC:212-243 / 247-345, which the reference runs without waiting for the agent) */
+#define FS_AUTORESET_SAME_STEP 0  /* gymnasium 0.29 SyncVectorEnv: obs = state(-1), final_* = terminal obs */
+#define FS_AUTORESET_NEXT_STEP 1  /* gymnasium 1.x: the step after a terminal one runs the burst only */
+
+/* fs_step flags */
+#define FS_ACT_HOST 0    /* action pointers are host memory (copied H2D on the handle's stream) */
+#define FS_ACT_DEVICE 1  /* action pointers are device memory */
+
+/* fs_reset flags */
+#define FS_RESET_HARD 0         /* RESET remote-control command (BC:143-146): Stop->Intro->Fight now */
+#define FS_RESET_IF_NEEDED 1    /* FootsiesEnv.reset (FE:482-515): RESET only arenas whose
+                                   has_terminated flag is clear; the others just finish the
+                                   pending KO->...->Fight burst (if any) and report state(-1) */
+
+typedef struct fs_config {
+  int32_t num_envs;        /* arenas on this handle (>0) */
+  int32_t device_id;       /* HIP device ordinal */
+  int32_t p2_mode;         /* FS_P2_* */
+  int32_t dense_reward;    /* 1: FE._get_dense_reward (FE:388-405, default FE:50); 0: sparse (FE:382-386) */
+  int32_t frame_delay;     /* FE:36,129-131; only 0 is supported */
+  int32_t float_mode;      /* FS_FLOAT_* */
+  int32_t autoreset_mode;  /* FS_AUTORESET_* */
+  int32_t reserved0;
+  uint64_t base_seed;      /* arena i's bot RNG is seeded with (int32)(base_seed + i) at creation
+                              (Random.InitState, BC:170-173) */
+} fs_config;
+
+/*
+ * Per-step outputs, struct-of-arrays, row i = arena i.  Pairs are [N][2]
+ * (column 0 = P1, column 1 = P2) exactly like FootsiesEnv's observation tuples
+ * (FE:360-368) stacked over arenas.
+ */
+typedef struct fs_outputs {
+  uint8_t* guard;        /* [N][2] obs["guard"]                       (FE:361)              */
+  uint8_t* move;         /* [N][2] obs["move"] = FOOTSIES_MOVE_ID_TO_INDEX, DEAD/WIN->STAND (FE:362-365, 537-549) */
+  float* move_frame;     /* [N][2] obs["move_frame"], 0 for STAND/FORWARD/BACKWARD (FE:339-358) */
+  float* position;       /* [N][2] obs["position"]                    (FE:367)              */
+  double* reward;        /* [N]    dense or sparse reward, float64 like FE (FE:382-405)     */
+  uint8_t* terminated;   /* [N]    p1Vital==0 or p2Vital==0           (FE:555)              */
+  uint8_t* truncated;    /* [N]    always 0                           (FE:569-570)          */
+  int32_t* frame;        /* [N]    info["frame"] = globalFrame        (FE:373)              */
+  uint8_t* action;       /* [N][2] info["p1_action"/"p2_action"] as 3-bit ints (Left=1, Right=2, Attack=4; state.py:26-36) */
+  uint8_t* hitstun;      /* [N][2] info["p1_hitstun"/"p2_hitstun"]   (FE:376-377)          */
+  /* FS_AUTORESET_SAME_STEP only: the terminal observation/info of arenas whose
+     terminated flag is set this step (other rows are left untouched) */
+  uint8_t* final_guard;      /* [N][2] */
+  uint8_t* final_move;       /* [N][2] */
+  float* final_move_frame;   /* [N][2] */
+  float* final_position;     /* [N][2] */
+  int32_t* final_frame;      /* [N]    */
+  uint8_t* final_action;     /* [N][2] */
+  uint8_t* final_hitstun;    /* [N][2] */
+} fs_outputs;
+
+/*
+ * Raw EnvironmentState of one arena (Assets/Script/EnvironmentState.cs:10-46,
+ * built by BattleCore.GetEnvironmentState, BC:449-468).  Used for state-level
+ * parity checks and for a wire-compatible JSON server.
+ */
+typedef struct fs_env_state {
+  int32_t p1Vital, p2Vital, p1Guard, p2Guard;
+  int32_t p1Move, p1MoveFrame, p2Move, p2MoveFrame;  /* raw actionIDs (0..510) */
+  float p1Position, p2Position;
+  int32_t globalFrame;
+  int32_t p1MostRecentAction, p2MostRecentAction;
+  int32_t p1Hitstun, p2Hitstun;
+} fs_env_state;
+
+/*
+ * Canonical full state of one arena: everything the simulation carries from one
+ * frame to the next (Fighter.cs:73-112, BC:56-70, BattleAI.cs:26-32), in a
+ * representation-independent form.  Both the HIP path and the CPU oracle export
+ * it, so lockstep tests compare hidden state, not only observations.
+ */
+typedef struct fs_fighter_state {
+  float position_x;
+  int32_t action_id;            /* raw actionID */
+  int32_t action_frame;
+  int32_t hit_count;
+  int32_t hitstun;
+  int32_t vital;
+  int32_t guard;
+  int32_t buffer_action_id;     /* -1 = none */
+  int32_t reserve_action_id;    /* -1 = none */
+  uint32_t input_dir_history;   /* Left/Right bits of input[0..15], 2 bits per frame, input[0] in bits 0-1 */
+  int32_t attack_hold;          /* consecutive frames input[0..] had Attack, saturating at 63 */
+  uint8_t is_input_backward;
+  uint8_t is_reserve_proximity_guard;
+  uint8_t has_won;
+  uint8_t pad0;
+} fs_fighter_state;
+
+typedef struct fs_arena_state {
+  fs_fighter_state f[2];
+  int32_t frame_count;          /* BattleCore.frameCount */
+  int32_t recording_count;      /* currentRecordingInputIndex, saturating at 18000 */
+  uint8_t recording_last[2];    /* recordingPnInput[index-1].input */
+  uint8_t actor_input[2];       /* TrainingActor.GetInput() values (stale inputs fed to the Intro tick) */
+  uint8_t reset_pending;        /* FS_AUTORESET_NEXT_STEP: terminal, burst not yet run */
+  uint8_t has_terminated;       /* FootsiesEnv.has_terminated (FE:191, 508, 563) */
+  uint8_t pad0[2];
+  double cumulative_reward;     /* FootsiesEnv._cummulative_episode_reward (FE:187) */
+  /* scripted bot (FS_P2_BOT) */
+  uint32_t rng[4];              /* UnityEngine.Random Xorshift128 state */
+  int32_t move_plan, move_index;     /* moveQueue as (plan id, dequeued count); plan -1 = empty */
+  int32_t attack_plan, attack_index; /* attackQueue likewise */
+  float prev_distance;          /* BattleAI.fightStates[5] (== previous call's state) */
+  int32_t prev_opponent_action; /* raw actionID of the opponent in that FightState */
+} fs_arena_state;
+
+typedef struct fs_context* fs_handle;
+
+/* Library / ABI version (FS_ABI_VERSION). */
+int fs_abi_version(void);
+
+/* Create N arenas on a device and run the game-start sequence (BattleCore.Start
+ * + first Stop->Intro->Fight ticks, BC:105-128, 176-200, 262-291) so they sit at
+ * state(-1).  Replaces FootsiesEnv.__init__ + _instantiate_game + _connect_to_game
+ * (FE:34-290).  Returns FS_E_UNSUPPORTED for frame_delay != 0. */
+int fs_create(const fs_config* cfg, fs_handle* out);
+
+/* Reset arenas (FootsiesEnv.reset, FE:482-515).  seeds: optional host array [N]
+ * -> Random.InitState((int32)seed) first (SEED command, BC:170-173; FE:487-488);
+ * mask: optional host array [N] of 0/1 selecting arenas (NULL = all); flags:
+ * FS_RESET_*.  Writes state(-1) observations of the reset arenas into the
+ * outputs (reward 0, terminated 0). */
+int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int flags);
+
+/* One Fight tick of every arena (FootsiesEnv.step, FE:518-570 -> BC:201-220,
+ * 347-364), with auto-reset of terminated arenas per cfg.autoreset_mode.
+ * p1_act: [N] 3-bit inputs (Left=1, Right=2, Attack=4; InputData.cs:8-14).
+ * p2_act: [N] for FS_P2_EXTERNAL, ignored (may be NULL) otherwise.
+ * flags: FS_ACT_HOST or FS_ACT_DEVICE for where the action arrays live. */
+int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags);
+
+/* n Fight ticks in one kernel launch (fused rollout).  Actions: device arrays
+ * [n][N], or NULL to draw them on device from the counter-based hash
+ * a = splitmix64(action_seed ^ env*0x9E3779B97F4A7C15 ^ (t << 1 | player)) & 7
+ * with t = fs_steps_taken(h) + k.  traj: device arrays laid out [n][N] (pairs
+ * [n][N][2]) receiving every tick's outputs; traj == NULL writes each tick
+ * into the handle's regular outputs (the last tick remains visible). */
+int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act,
+              uint64_t action_seed, const fs_outputs* traj);
+
+/* Device pointers of the current outputs, valid until the next call on h. */
+int fs_outputs_get(fs_handle h, fs_outputs* out);
+
+/* Redirect the per-step outputs into caller-owned device buffers (e.g. torch
+ * tensors) for zero-copy; NULL members keep the library's own buffer.  The
+ * buffers must stay alive until fs_destroy or the next bind. */
+int fs_bind_outputs(fs_handle h, const fs_outputs* dev);
+
+/* Copy the raw EnvironmentState [N] / canonical full state [N] of every arena
+ * to host memory (synchronous).  fs_get_state replaces STATE_SAVE
+ * (BC:148-151, 667-674) in canonical form. */
+int fs_get_env_state(fs_handle h, fs_env_state* host_out);
+int fs_get_state(fs_handle h, fs_arena_state* host_out);
+/* Load canonical state [N] from host (STATE_LOAD, BC:153-156, 676-683).
+ * Input history beyond what fs_arena_state carries is not representable. */
+int fs_set_state(fs_handle h, const fs_arena_state* host_in);
+
+/* Block until all work on the handle's stream is done. */
+int fs_sync(fs_handle h);
+/* The handle's hipStream_t (as void*), for event timing / torch.cuda.ExternalStream. */
+void* fs_stream(fs_handle h);
+/* Run all further work of h on a caller-owned hipStream_t (e.g. PyTorch's current
+ * stream; NULL = the HIP null stream) instead of the library's own, so device
+ * actions/outputs are ordered with the caller's kernels without events.
+ * FS_STREAM_OWN restores the library's stream.  The caller keeps the stream
+ * alive while h uses it; switching orders the new stream after the old one. */
+#define FS_STREAM_OWN ((void*)(intptr_t)-1)
+int fs_set_stream(fs_handle h, void* stream);
+int fs_num_envs(fs_handle h);
+uint64_t fs_steps_taken(fs_handle h);
+void fs_destroy(fs_handle h);
+/* Last error message of h (or of the last failed fs_create when h is NULL). */
+const char* fs_last_error(fs_handle h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FOOTSIES_H */

@@ -1,0 +1,83 @@
+"""HIP path (libfootsies.so through FootsiesSim) vs the CPU oracle, in lockstep.
+
+Bit-exact on every output and on the canonical hidden state (fs_get_state).
+"""
+import numpy as np
+import pytest
+
+from footsies_gym_amd import _abi
+from tests.parity_utils import compare_outputs, compare_states
+
+pytestmark = pytest.mark.gpu
+
+P2 = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT, "noop": _abi.FS_P2_NOOP}
+FM = {"strict": _abi.FS_FLOAT_STRICT32, "double": _abi.FS_FLOAT_DOUBLE}
+AR = {"same_step": _abi.FS_AUTORESET_SAME_STEP, "next_step": _abi.FS_AUTORESET_NEXT_STEP}
+
+
+def make_pair(oracle_lib, n, p2, fm="strict", ar="same_step", dense=True, seed=0):
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(n, p2_mode=p2, float_mode=fm, autoreset_mode=ar, dense_reward=dense, seed=seed)
+    ora = oracle_lib.Oracle(n, p2_mode=P2[p2], float_mode=FM[fm], autoreset_mode=AR[ar], dense_reward=dense,
+                            base_seed=seed)
+    return sim, ora
+
+
+def run_lockstep(sim, ora, steps, rng, state_every=50, sticky=0.0):
+    n = sim.num_envs
+    compare_outputs(ora.outputs(), sim.outputs_numpy(), step=-1)
+    compare_states(ora.state(), sim.get_state(), step=-1)
+    a1 = rng.integers(0, 8, n).astype(np.uint8)
+    a2 = rng.integers(0, 8, n).astype(np.uint8)
+    for t in range(steps):
+        # sticky random actions exercise holds (charge specials), dashes and walks
+        keep = rng.random(n) < sticky
+        a1 = np.where(keep, a1, rng.integers(0, 8, n)).astype(np.uint8)
+        keep = rng.random(n) < sticky
+        a2 = np.where(keep, a2, rng.integers(0, 8, n)).astype(np.uint8)
+        eo = ora.step(a1, a2 if sim.p2_mode == "external" else None)
+        go = sim.step(a1, a2 if sim.p2_mode == "external" else None)
+        go = sim.outputs_numpy()
+        compare_outputs(eo, go, step=t, same_step=sim.autoreset_mode == "same_step")
+        if state_every and (t % state_every == 0 or t == steps - 1):
+            compare_states(ora.state(), sim.get_state(), step=t)
+
+
+@pytest.mark.parametrize("p2", ["external", "bot", "noop"])
+def test_lockstep_random(oracle_lib, p2):
+    sim, ora = make_pair(oracle_lib, 512, p2, seed=11)
+    run_lockstep(sim, ora, 600, np.random.default_rng(1), sticky=0.0)
+
+
+@pytest.mark.parametrize("p2", ["external", "bot"])
+def test_lockstep_sticky(oracle_lib, p2):
+    sim, ora = make_pair(oracle_lib, 512, p2, seed=5)
+    run_lockstep(sim, ora, 800, np.random.default_rng(2), sticky=0.9)
+
+
+@pytest.mark.parametrize("fm,ar,dense", [("double", "same_step", True), ("strict", "next_step", True),
+                                          ("strict", "same_step", False), ("double", "next_step", False)])
+def test_lockstep_modes(oracle_lib, fm, ar, dense):
+    sim, ora = make_pair(oracle_lib, 256, "bot", fm=fm, ar=ar, dense=dense, seed=3)
+    run_lockstep(sim, ora, 500, np.random.default_rng(3), sticky=0.7)
+
+
+def test_resets_lockstep(oracle_lib):
+    sim, ora = make_pair(oracle_lib, 256, "bot", seed=9)
+    rng = np.random.default_rng(4)
+    for rnd in range(6):
+        run_lockstep(sim, ora, 60, rng, state_every=20, sticky=0.5)
+        mask = (rng.random(256) < 0.5).astype(np.uint8)
+        seeds = rng.integers(0, 2**31, 256).astype(np.uint64) if rnd % 2 else None
+        hard = rnd % 3 == 0
+        flags = _abi.FS_RESET_HARD if hard else _abi.FS_RESET_IF_NEEDED
+        eo = ora.reset(seeds=seeds, mask=mask, flags=flags)
+        sim.reset(seeds=seeds, mask=mask, hard=hard)
+        compare_outputs(eo, sim.outputs_numpy(), step=-2)
+        compare_states(ora.state(), sim.get_state(), step=-2)
+
+
+def test_lockstep_4096_bot_long(oracle_lib):
+    """Config 2 shape: 4096 arenas, random P1 vs scripted bot P2, 10k steps."""
+    sim, ora = make_pair(oracle_lib, 4096, "bot", seed=0)
+    run_lockstep(sim, ora, 10000, np.random.default_rng(123), state_every=500, sticky=0.5)
