@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py -- env-steps/sec of the FOOTSIES hot path on MI355X (BASELINE.json's metric).
+
+Workload (BASELINE.json configs[2], "C3"): 65 536 arenas per GPU, self-play with
+synthetic random actions for both players (the splitmix64 stream of SURVEY.md
+§8(d), generated into HBM by fs_hash_actions before the timed region).  One
+"step" = one Fight tick of every arena with full per-step outputs (obs, reward,
+terminated/truncated, info) written to HBM and auto-reset of finished episodes
+-- exactly FootsiesEnv.step's work for all arenas.
+
+Modes
+  fused (default): fs_step_n, `--chunk` ticks per kernel launch, every tick's
+                   outputs kept in a [chunk][N] rollout buffer in HBM.
+  step:            fs_step, one kernel launch per tick (the VectorEnv.step path).
+Both modes are timed and reported; `value` is the --mode one.
+
+Multi-GPU: one process per GPU (torch.distributed.run), arenas sharded per rank
+with no data-path collective (`scaling: weak`); max-over-ranks timing.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node) at 65 536 envs; bit-exact vs Unity ref"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (8.0 TB/s spec)
+STATE_BYTES = 96        # per arena per launch: 48 B state read + 48 B written (fs_kernels.hip layout)
+STEP_IO_BYTES = 40      # per env-step: 2 B actions in + 38 B outputs out (include/footsies.h fs_outputs)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=65536, help="arenas per GPU")
+    ap.add_argument("--mode", choices=["fused", "step"], default="fused")
+    ap.add_argument("--chunk", type=int, default=100, help="ticks per fs_step_n launch (fused mode)")
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-samples", type=int, default=50, help="launches timed back-to-back for roofline")
+    return ap.parse_args()
+
+
+def cpu_baseline(envs, seconds, seed):
+    """The CPU oracle (scalar C port, OpenMP over host cores) on a bounded sample."""
+    from oracle import binding
+    from footsies_gym_amd import _abi
+    binding.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    binding.lib().or_set_threads(threads)
+    threads = binding.lib().or_get_threads()
+    o = binding.Oracle(envs, p2_mode=_abi.FS_P2_EXTERNAL, base_seed=0)
+    o.step_n_hashed(5, seed)  # warm-up / page-in
+    t = time.perf_counter()
+    o.step_n_hashed(10, seed)
+    probe = time.perf_counter() - t
+    steps = int(max(10, min(5000, seconds / max(probe / 10, 1e-9))))
+    t = time.perf_counter()
+    o.step_n_hashed(steps, seed)
+    dt = time.perf_counter() - t
+    o.close()
+    return {"value": envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "%d arenas x %d steps, self-play splitmix64 actions, oracle/liboracle.so (OpenMP %d threads), "
+                      "%.1f s" % (envs, steps, threads, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from footsies_gym_amd import _abi
+    from footsies_gym_amd._lib import check, lib
+    from footsies_gym_amd.simulator import FootsiesSim
+
+    N, K, W = args.envs, args.steps, args.warmup
+    sim = FootsiesSim(N, device=local, p2_mode="external", seed=rank * N)
+    h = sim.handle
+    L = lib()
+    # synthetic inputs resident in HBM before timing
+    p1, p2 = sim.hash_actions(W + K, seed=args.seed, t0=0)
+    torch.cuda.synchronize(dev)
+    base1, base2 = p1.data_ptr(), p2.data_ptr()
+    chunk = max(1, min(args.chunk, K))
+    traj = sim.alloc_trajectory(chunk)
+    tdesc = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+    fs_step, fs_step_n = L.fs_step, L.fs_step_n
+
+    def run_step(k0, n):
+        for k in range(k0, k0 + n):
+            rc = fs_step(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE)
+            if rc:
+                check(rc, h)
+
+    def run_fused(k0, n):
+        k = k0
+        while k < k0 + n:
+            m = min(chunk, k0 + n - k)
+            rc = fs_step_n(h, m, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), 0, C.byref(tdesc))
+            if rc:
+                check(rc, h)
+            k += m
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def timed(fn, k0, n):
+        barrier()
+        torch.cuda.synchronize(dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        fn(k0, n)
+        ev1.record()
+        torch.cuda.synchronize(dev)
+        barrier()
+        wall = time.perf_counter() - t0
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), ev0.elapsed_time(ev1) / 1e3
+
+    def kernel_time(fn, k0, launches, ticks_per_launch):
+        """Average kernel duration with the queue pre-filled (a spin kernel holds the GPU while
+        the host enqueues), so event pairs bracket back-to-back kernels, not host gaps."""
+        torch.cuda.synchronize(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+        try:
+            torch.cuda._sleep(int(2e7))
+        except Exception:
+            pass
+        for j, (a, b) in enumerate(evs):
+            a.record()
+            fn(k0 + (j * ticks_per_launch) % max(1, K - ticks_per_launch), ticks_per_launch)
+            b.record()
+        torch.cuda.synchronize(dev)
+        d = sorted(a.elapsed_time(b) / 1e3 for a, b in evs)
+        return sum(d) / len(d), d[len(d) // 2]
+
+    # warm-up (untimed)
+    if W:
+        (run_fused if args.mode == "fused" else run_step)(0, W)
+    torch.cuda.synchronize(dev)
+
+    res = {}
+    for mode, fn in (("fused", run_fused), ("step", run_step)):
+        wall, ev = timed(fn, W, K)
+        res[mode] = {"wall_s": wall, "event_s": ev, "env_steps_per_s": world * N * K / wall,
+                     "ms_per_step": 1e3 * wall / K}
+    # dominant kernel of the reported mode, back-to-back launches
+    if args.mode == "fused":
+        kt, kmed = kernel_time(run_fused, W, max(5, args.kernel_samples // 10), chunk)
+        bytes_per_launch = N * (STATE_BYTES + chunk * STEP_IO_BYTES)
+    else:
+        kt, kmed = kernel_time(run_step, W, args.kernel_samples, 1)
+        bytes_per_launch = N * (STATE_BYTES + STEP_IO_BYTES)
+    achieved = bytes_per_launch / kt / 1e9
+    other = "step" if args.mode == "fused" else "fused"
+    out = {
+        "metric": METRIC,
+        "value": res[args.mode]["env_steps_per_s"],
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": res[args.mode]["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32+f32 (reward f64)",
+        "data": "synthetic (splitmix64 self-play actions in HBM)",
+        "config": {"workload": "C3: %d arenas/GPU, self-play random actions, P2 external, auto-reset same-step" % N,
+                   "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
+                   "ticks_per_launch": chunk if args.mode == "fused" else 1, "parallelism": "arena-shard x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": "fsk::k_step<0,0>", "avg_launch_us": kt * 1e6, "median_launch_us": kmed * 1e6,
+                     "algorithmic_bytes_per_launch": bytes_per_launch},
+        other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)
+    if rank == 0:
+        print(json.dumps(out))
+    sim.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,8 +17,11 @@ SOURCES = ["fs_kernels.hip", "fs_api.cpp"]
 HEADERS = ["fs_internal.h", "fs_tables.h"]
 
 # -ffp-contract=off: no a*b+c fusion -- every float op must round like the C# it restates.
+# -simplifycfg-sink-common=false: SimplifyCFG otherwise sinks the per-branch field stores
+#   of the action state machine into one store through a pointer phi, which blocks SROA and
+#   leaves the whole per-lane arena (272 B) in scratch memory -- 400+ scratch ops per tick.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
-          "-fno-fast-math", "-Wall", "-Wno-unused-function"]
+          "-fno-fast-math", "-Wall", "-Wno-unused-function", "-mllvm", "-simplifycfg-sink-common=false"]
 
 
 def _hipcc():

@@ -308,6 +308,14 @@ FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p
   return step_common(h, n, p1_act, p2_act, FS_ACT_DEVICE, action_seed, traj);
 }
 
+FS_API int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out) {
+  if (!h || !p1_out || n_steps <= 0) return FS_E_INVALID;
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  HIP_TRY(h, fsk::launch_hash_actions(h->n, n_steps, seed, t0, p1_out, p2_out, h->stream));
+  return FS_OK;
+}
+
 FS_API int fs_outputs_get(fs_handle h, fs_outputs* o) {
   if (!h || !o) return FS_E_INVALID;
   const fsk::DevOutputs& d = h->out;

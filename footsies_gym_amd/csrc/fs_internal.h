@@ -68,6 +68,8 @@ struct ResetParams {
 // launchers (fs_kernels.hip); return hipError_t of the launch
 hipError_t launch_step(const StepParams& p, int float_mode, int p2_mode, hipStream_t s);
 hipError_t launch_reset(const ResetParams& p, int float_mode, int p2_mode, hipStream_t s);
+hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1, uint8_t* p2,
+                               hipStream_t s);
 hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_state* env_dst, int n, int p2_mode,
                             hipStream_t s);
 hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, int p2_mode, hipStream_t s);

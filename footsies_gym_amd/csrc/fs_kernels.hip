@@ -32,6 +32,38 @@ constexpr int NONE = 31;  // empty buffer / reserve slot
 constexpr uint32_t IN_LEFT = 1, IN_RIGHT = 2, IN_ATTACK = 4;
 
 // ---------------------------------------------------------------------------
+// frame data staged in LDS.  Every lookup of the tick (action info -> row ->
+// box / velocity / cancel records) is a dependent, lane-divergent load; from
+// LDS it costs ~tens of cycles instead of an L1/L2 round trip.  ~4.3 KB per
+// block, copied once per launch by all threads of the block.
+// ---------------------------------------------------------------------------
+struct Tables {
+  ActionInfo action[kNumActions];
+  uint32_t rows[kNumRows];
+  float4 rects[kNumRects];
+  float vels[kNumVels];
+  uint32_t hitsets[kNumHitSets];
+  uint32_t hurtsets[kNumHurtSets];
+  uint32_t cancel[kNumCancelMasks];
+  AttackInfo attacks[4];
+};
+__shared__ Tables sT;
+
+// all threads of the block must call this before any early return
+__device__ __forceinline__ void stage_tables() {
+  const int t = threadIdx.x, nt = blockDim.x;
+  for (int i = t; i < kNumRows; i += nt) sT.rows[i] = kRows[i];
+  for (int i = t; i < kNumActions; i += nt) sT.action[i] = kActionInfo[i];
+  for (int i = t; i < kNumRects; i += nt) sT.rects[i] = kRects[i];
+  for (int i = t; i < kNumVels; i += nt) sT.vels[i] = kVels[i];
+  for (int i = t; i < kNumHitSets; i += nt) sT.hitsets[i] = kHitSets[i];
+  for (int i = t; i < kNumHurtSets; i += nt) sT.hurtsets[i] = kHurtSets[i];
+  for (int i = t; i < kNumCancelMasks; i += nt) sT.cancel[i] = kCancelMasks[i];
+  for (int i = t; i < 4; i += nt) sT.attacks[i] = kAttacks[i];
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
 // packed fighter word (u64), one per fighter in DevState::fpk
 //   [0,5) action idx | [5,14) action frame | [14,19) hitstun | [19,21) vital |
 //   [21,23) guard | [23,25) hit count | [25,30) buffer idx | [30,35) reserve idx |
@@ -56,7 +88,7 @@ struct Fighter {
 };
 
 struct Arena {
-  Fighter f[2];
+  Fighter f0, f1;
   int frame_count;
   uint32_t rec_count, rec1, rec2, act1, act2;
   bool pending, has_term;
@@ -96,12 +128,12 @@ __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
   uint4 pk = s.fpk[i];
   int2 aw = s.aw[i];
   A.cum = s.cum[i];
-  unpack_fighter(A.f[0], pk.x, pk.y);
-  unpack_fighter(A.f[1], pk.z, pk.w);
-  A.f[0].x = pos.x;
-  A.f[1].x = pos.y;
-  A.f[0].hist = hist.x;
-  A.f[1].hist = hist.y;
+  unpack_fighter(A.f0, pk.x, pk.y);
+  unpack_fighter(A.f1, pk.z, pk.w);
+  A.f0.x = pos.x;
+  A.f1.x = pos.y;
+  A.f0.hist = hist.x;
+  A.f1.hist = hist.y;
   A.frame_count = aw.x;
   uint32_t h = (uint32_t)aw.y;
   A.rec_count = h & 0x7fff;
@@ -125,9 +157,9 @@ __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
 
 template <bool BOT>
 __device__ __forceinline__ void store_arena(const Arena& A, const DevState& s, int i) {
-  uint64_t w0 = pack_fighter(A.f[0]), w1 = pack_fighter(A.f[1]);
-  s.pos[i] = make_float2(A.f[0].x, A.f[1].x);
-  s.hist[i] = make_uint2(A.f[0].hist, A.f[1].hist);
+  uint64_t w0 = pack_fighter(A.f0), w1 = pack_fighter(A.f1);
+  s.pos[i] = make_float2(A.f0.x, A.f1.x);
+  s.hist[i] = make_uint2(A.f0.hist, A.f1.hist);
   s.fpk[i] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   uint32_t h = A.rec_count | (A.rec1 << 15) | (A.rec2 << 18) | (A.act1 << 21) | (A.act2 << 24) |
                ((uint32_t)A.pending << 27) | ((uint32_t)A.has_term << 28);
@@ -252,7 +284,7 @@ __device__ __forceinline__ void set_action(Fighter& f, int a) {
 }
 
 __device__ __forceinline__ void request_action(Fighter& f, int a) {
-  const ActionInfo ai = kActionInfo[f.act];
+  const ActionInfo ai = sT.action[f.act];
   if (f.frame >= ai.frame_count) {
     set_action(f, a);
     return;
@@ -262,8 +294,8 @@ __device__ __forceinline__ void request_action(Fighter& f, int a) {
     set_action(f, a);
     return;
   }
-  const uint32_t row = kRows[ai.row + f.frame];
-  if (kCancelMasks[(row >> 21) & 15] & (1u << a)) f.buf = a;  // buffer or execute window lists `a`
+  const uint32_t row = sT.rows[ai.row + f.frame];
+  if (sT.cancel[(row >> 21) & 15] & (1u << a)) f.buf = a;  // buffer or execute window lists `a`
 }
 
 __device__ __forceinline__ void increment_action_frame(Fighter& f) {
@@ -272,7 +304,7 @@ __device__ __forceinline__ void increment_action_frame(Fighter& f) {
     return;
   }
   f.frame++;
-  const ActionInfo ai = kActionInfo[f.act];
+  const ActionInfo ai = sT.action[f.act];
   if (f.frame >= ai.frame_count && ai.loop_from >= 0) f.frame = ai.loop_from;
 }
 
@@ -281,18 +313,20 @@ __device__ __forceinline__ void update_action_request(Fighter& f, const InputEva
     request_action(f, A_WIN);
     return;
   }
-  if (f.rsv != NONE && f.stun <= 0) {
-    set_action(f, f.rsv);
-    return;
-  }
-  if (f.buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0) {
-    set_action(f, f.buf);
+  // reserved damage action, then buffered cancel (F:212-229).  Written as a value
+  // select so the compiler cannot merge the two tails into a pointer phi (which
+  // would pin the whole arena in scratch memory).
+  const int rsv = f.rsv, buf = f.buf;
+  const bool take_rsv = rsv != NONE && f.stun <= 0;
+  const bool take_buf = !take_rsv && buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0;
+  if (take_rsv || take_buf) {
+    set_action(f, take_rsv ? rsv : buf);
     return;
   }
   if (e.special) {
     request_action(f, (e.fwd || e.back) ? A_B_SPECIAL : A_N_SPECIAL);
   } else if (e.atk_down) {
-    if ((f.act == A_N_ATTACK || f.act == A_B_ATTACK) && f.frame < kActionInfo[f.act].frame_count)
+    if ((f.act == A_N_ATTACK || f.act == A_B_ATTACK) && f.frame < sT.action[f.act].frame_count)
       request_action(f, A_N_SPECIAL);
     else
       request_action(f, (e.fwd || e.back) ? A_B_ATTACK : A_N_ATTACK);
@@ -315,9 +349,9 @@ __device__ __forceinline__ void update_movement(Fighter& f, float sign) {
   } else if (f.act == A_BACKWARD) {
     f.x = pos_minus_vel<FM>(f.x, kBackwardSpeed, sign);
   } else {
-    const uint32_t vi = kRows[kActionInfo[f.act].row + f.frame] & 15;
+    const uint32_t vi = sT.rows[sT.action[f.act].row + f.frame] & 15;
     if (vi) {
-      const float v = kVels[vi];
+      const float v = sT.vels[vi];
       if (v != 0.0f) f.x = pos_plus_vel<FM>(f.x, v, sign);
     }
   }
@@ -325,15 +359,15 @@ __device__ __forceinline__ void update_movement(Fighter& f, float sign) {
 
 template <int FM>
 __device__ __forceinline__ void update_boxes(Fighter& f, float sign) {
-  const uint32_t row = kRows[kActionInfo[f.act].row + f.frame];
+  const uint32_t row = sT.rows[sT.action[f.act].row + f.frame];
   f.push_rect = (row >> 4) & 31;
-  f.hurtset = kHurtSets[(row >> 9) & 63];
-  f.hitset = kHitSets[(row >> 15) & 63];
-  f.px = xform<FM>(f.x, kRects[f.push_rect].x, sign);
-  f.ux0 = xform<FM>(f.x, kRects[(f.hurtset >> 2) & 63].x, sign);
-  f.ux1 = xform<FM>(f.x, kRects[(f.hurtset >> 8) & 63].x, sign);
-  f.hx0 = xform<FM>(f.x, kRects[(f.hitset >> 2) & 63].x, sign);
-  f.hx1 = xform<FM>(f.x, kRects[(f.hitset >> 11) & 63].x, sign);
+  f.hurtset = sT.hurtsets[(row >> 9) & 63];
+  f.hitset = sT.hitsets[(row >> 15) & 63];
+  f.px = xform<FM>(f.x, sT.rects[f.push_rect].x, sign);
+  f.ux0 = xform<FM>(f.x, sT.rects[(f.hurtset >> 2) & 63].x, sign);
+  f.ux1 = xform<FM>(f.x, sT.rects[(f.hurtset >> 8) & 63].x, sign);
+  f.hx0 = xform<FM>(f.x, sT.rects[(f.hitset >> 2) & 63].x, sign);
+  f.hx1 = xform<FM>(f.x, sT.rects[(f.hitset >> 11) & 63].x, sign);
 }
 
 // ApplyPositionChange (F:331-350): position and every box are shifted, not rebuilt
@@ -351,7 +385,7 @@ __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
 // x is xMin, xMax = width + x, Overlaps is strict.
 template <int FM>
 __device__ __forceinline__ void push_character_vs_character(Fighter& a, Fighter& b) {
-  const float4 ra = kRects[a.push_rect], rb = kRects[b.push_rect];
+  const float4 ra = sT.rects[a.push_rect], rb = sT.rects[b.push_rect];
   const float a_xmax = fadd<FM>(ra.z, a.px), b_xmax = fadd<FM>(rb.z, b.px);
   const float a_ymax = fadd<FM>(ra.w, ra.y), b_ymax = fadd<FM>(rb.w, rb.y);
   const bool overlap = b_xmax > a.px && b.px < a_xmax && b_ymax > ra.y && rb.y < a_ymax;
@@ -388,7 +422,7 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& a, Fighter&
 // UpdatePushCharacterVsBackground (BC:503-519) with BoxBase semantics
 template <int FM>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
-  const float w = kRects[f.push_rect].z;
+  const float w = sT.rects[f.push_rect].z;
   const float xmin = bb_xmin<FM>(f.px, w);
   if (xmin < -kStageHalf) {
     apply_position_change<FM>(f, fsub<FM>(-kStageHalf, xmin));
@@ -420,7 +454,7 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
       f.guard = 0;
     }
   }
-  if (f.act == A_BACKWARD || kActionInfo[f.act].guard_type) {
+  if (f.act == A_BACKWARD || sT.action[f.act].guard_type) {
     set_action(f, ad.guard_action);
     if (guard_break) {
       f.rsv = A_GUARD_BREAK;
@@ -447,11 +481,11 @@ __device__ __forceinline__ void collide(Fighter& att, Fighter& def) {
   for (int h = 0; h < nh; h++) {
     const uint32_t hb = (att.hitset >> (2 + 9 * h)) & 511;
     const int aidx = (hb >> 6) & 3;
-    if (att.hits >= kAttacks[aidx].number_of_hit) continue;  // CanAttackHit (F:408-420)
-    const float4 hr = kRects[hb & 63];
+    if (att.hits >= sT.attacks[aidx].number_of_hit) continue;  // CanAttackHit (F:408-420)
+    const float4 hr = sT.rects[hb & 63];
     const float hx = h == 0 ? att.hx0 : att.hx1;
     for (int u = 0; u < nu; u++) {
-      const float4 ur = kRects[(def.hurtset >> (2 + 6 * u)) & 63];
+      const float4 ur = sT.rects[(def.hurtset >> (2 + 6 * u)) & 63];
       const float ux = u == 0 ? def.ux0 : def.ux1;
       if (box_overlaps<FM>(hx, hr, ux, ur)) {
         if ((hb >> 8) & 1) {
@@ -467,7 +501,7 @@ __device__ __forceinline__ void collide(Fighter& att, Fighter& def) {
   }
   if (hit) {
     att.hits++;  // NotifyAttackHit (F:352-355)
-    const AttackInfo ad = kAttacks[atk];
+    const AttackInfo ad = sT.attacks[atk];
     const int res = notify_damaged(def, ad);
     const int stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
     att.stun = stun;  // SetHitStun on both (BC:576-578)
@@ -482,8 +516,14 @@ __device__ __forceinline__ void collide(Fighter& att, Fighter& def) {
 // ---------------------------------------------------------------------------
 enum { MP_NEUTRAL, MP_FAR1, MP_FAR2, MP_MID1, MP_MID2, MP_FALLBACK1, MP_FALLBACK2 };
 enum { AP_NONE, AP_ONE_HIT, AP_TWO_HIT, AP_IMMEDIATE_SPECIAL, AP_DELAY_SPECIAL };
-__constant__ const uint8_t kMovePlanLen[7] = {30, 90, 56, 70, 33, 60, 63};
-__constant__ const uint8_t kAttackPlanLen[5] = {30, 19, 23, 61, 121};
+__device__ __forceinline__ uint32_t move_plan_len(uint32_t plan) {  // AI:192-253
+  return plan == MP_FAR1 ? 90u : plan == MP_FAR2 ? 56u : plan == MP_MID1 ? 70u : plan == MP_MID2 ? 33u
+       : plan == MP_FALLBACK1 ? 60u : plan == MP_FALLBACK2 ? 63u : 30u;
+}
+__device__ __forceinline__ uint32_t attack_plan_len(uint32_t plan) {  // AI:255-312
+  return plan == AP_ONE_HIT ? 19u : plan == AP_TWO_HIT ? 23u : plan == AP_IMMEDIATE_SPECIAL ? 61u
+       : plan == AP_DELAY_SPECIAL ? 121u : 30u;
+}
 
 __device__ __forceinline__ uint32_t rng_next(uint4& s) {  // UnityEngine.Random Xorshift128
   const uint32_t t = s.x ^ (s.x << 11);
@@ -571,14 +611,14 @@ __device__ __forceinline__ uint32_t select_attack(uint4& rng, float d, uint32_t 
 
 template <int FM>
 __device__ __forceinline__ float bot_distance(const Arena& A) {  // Mathf.Abs(f2.x - f1.x) (AI:370-373)
-  return fabsf(fsub<FM>(A.f[1].x, A.f[0].x));
+  return fabsf(fsub<FM>(A.f1.x, A.f0.x));
 }
 
 template <int FM>
 __device__ __forceinline__ void bot_reset(Arena& A) {  // AI:393-403
   A.mplan = A.midx = A.aplan = A.aidx = 0;
   A.prev_dist = bot_distance<FM>(A);
-  A.prev_opp = A.f[0].act;
+  A.prev_opp = A.f0.act;
 }
 
 // getNextAIInput (AI:41-66).  The ascending copy loop of UpdateFightState
@@ -588,18 +628,18 @@ __device__ __forceinline__ uint32_t bot_next_input(Arena& A) {
   const float d = A.prev_dist;
   const uint32_t opp = A.prev_opp;
   A.prev_dist = bot_distance<FM>(A);
-  A.prev_opp = A.f[0].act;
+  A.prev_opp = A.f0.act;
   uint32_t input = 0;
   if (A.mplan) {
     input |= move_plan_input(A.mplan - 1, A.midx);
-    if (++A.midx == kMovePlanLen[A.mplan - 1]) A.mplan = 0;
+    if (++A.midx == move_plan_len(A.mplan - 1)) A.mplan = 0;
   } else {
     A.mplan = select_movement(A.rng, d) + 1;
     A.midx = 0;
   }
   if (A.aplan) {
     input |= attack_plan_input(A.aplan - 1, A.aidx);
-    if (++A.aidx == kAttackPlanLen[A.aplan - 1]) A.aplan = 0;
+    if (++A.aidx == attack_plan_len(A.aplan - 1)) A.aplan = 0;
   } else {
     A.aplan = select_attack(A.rng, d, opp) + 1;
     A.aidx = 0;
@@ -619,13 +659,13 @@ __device__ __forceinline__ void record_input(Arena& A, uint32_t p1, uint32_t p2)
 
 template <int FM>
 __device__ __forceinline__ void physics_tail(Arena& A) {  // movement, boxes, pushes (shared by all tick kinds)
-  update_movement<FM>(A.f[0], 1.0f);
-  update_movement<FM>(A.f[1], -1.0f);
-  update_boxes<FM>(A.f[0], 1.0f);
-  update_boxes<FM>(A.f[1], -1.0f);
-  push_character_vs_character<FM>(A.f[0], A.f[1]);
-  push_character_vs_background<FM>(A.f[0]);
-  push_character_vs_background<FM>(A.f[1]);
+  update_movement<FM>(A.f0, 1.0f);
+  update_movement<FM>(A.f1, -1.0f);
+  update_boxes<FM>(A.f0, 1.0f);
+  update_boxes<FM>(A.f1, -1.0f);
+  push_character_vs_character<FM>(A.f0, A.f1);
+  push_character_vs_background<FM>(A.f0);
+  push_character_vs_background<FM>(A.f1);
 }
 
 // UpdateFightState (BC:347-364); returns battleOver (BC:212-213)
@@ -633,21 +673,21 @@ template <int FM>
 __device__ __forceinline__ bool fight_tick(Arena& A) {
   A.frame_count++;
   record_input(A, A.act1, A.act2);
-  const InputEval e0 = update_input(A.f[0], A.act1, 0);
-  const InputEval e1 = update_input(A.f[1], A.act2, 1);
-  increment_action_frame(A.f[0]);
-  increment_action_frame(A.f[1]);
-  update_action_request(A.f[0], e0);
-  update_action_request(A.f[1], e1);
+  const InputEval e0 = update_input(A.f0, A.act1, 0);
+  const InputEval e1 = update_input(A.f1, A.act2, 1);
+  increment_action_frame(A.f0);
+  increment_action_frame(A.f1);
+  update_action_request(A.f0, e0);
+  update_action_request(A.f1, e1);
   physics_tail<FM>(A);
-  collide<FM>(A.f[0], A.f[1]);
-  collide<FM>(A.f[1], A.f[0]);
-  return A.f[0].vital <= 0 || A.f[1].vital <= 0;
+  collide<FM>(A.f0, A.f1);
+  collide<FM>(A.f1, A.f0);
+  return A.f0.vital <= 0 || A.f1.vital <= 0;
 }
 
 __device__ __forceinline__ void ko_clear_input(Arena& A) {  // ChangeRoundState(KO): ClearInput (BC:292-299)
-  A.f[0].hist = A.f[1].hist = 0;
-  A.f[0].hold = A.f[1].hold = 0;
+  A.f0.hist = A.f1.hist = 0;
+  A.f0.hold = A.f1.hold = 0;
 }
 
 __device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {  // F:120-135
@@ -660,38 +700,54 @@ __device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {  // F:
   set_action(f, A_STAND);
 }
 
-// KO tick -> End (winner), End tick (BC:221-243, 306-325, 371-381)
-template <int FM>
-__device__ __forceinline__ void ko_and_end_ticks(Arena& A) {
-  const bool d0 = A.f[0].vital <= 0, d1 = A.f[1].vital <= 0;
-  if (d0 != d1) {
-    if (d0) A.f[1].won = true;
-    else A.f[0].won = true;
-  }
-  increment_action_frame(A.f[0]);
-  increment_action_frame(A.f[1]);
-  const InputEval none = {false, false, false, false, false, false};  // histories were cleared at KO
-  update_action_request(A.f[0], none);
-  update_action_request(A.f[1], none);
-  physics_tail<FM>(A);
+// KO tick -> End (winner), End tick (BC:221-243, 306-325, 371-381), reduced to
+// its observable effects.  The End tick runs IncrementActionFrame,
+// UpdateActionRequest, movement, boxes and pushes, but SetupBattleStart (next
+// tick) overwrites position, action, frame, hit count, buffer, reserve, vital,
+// guard, hasWon and the input history.  What survives is (a) the hitstun
+// decrement and (b) UpdateActionRequest clearing isInputBackward /
+// isReserveProximityGuard -- which it does unless it returned early: for the
+// winner (hasWon), or on the reserve / buffer paths (F:204-229).  The input
+// history was cleared at KO, so the fall-through path sees no input.
+__device__ __forceinline__ void end_tick_effects(Fighter& f, bool won) {
+  const bool stunned = f.stun > 0;
+  f.stun -= stunned ? 1 : 0;  // IncrementActionFrame (F:150-154); the frame itself is overwritten
+  const bool early = won || (f.rsv != NONE && f.stun <= 0) ||
+                     (f.buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0);
+  f.in_back = early ? f.in_back : false;
+  f.prox = early ? f.prox : false;
 }
 
-// Stop tick -> Intro (setup, bot Reset), Intro tick with the stale actor inputs,
-// -> Fight (frameCount = -1) and the state(-1) emission with the bot's request
-// (BC:178-200, 262-291, 329-345)
+__device__ __forceinline__ void ko_and_end_ticks(Arena& A) {
+  const bool d0 = A.f0.vital <= 0, d1 = A.f1.vital <= 0;
+  end_tick_effects(A.f0, A.f0.won || (d1 && !d0));  // a sole survivor gets RequestWinAction (BC:310-323)
+  end_tick_effects(A.f1, A.f1.won || (d0 && !d1));
+}
+
+// Intro tick for one fighter right after SetupBattleStart (BC:329-345): the stale
+// actor input enters the cleared history, the frame advances unless in hitstun,
+// and RequestAction(STAND) on STAND is a no-op.  Movement, boxes and both pushes
+// are no-ops here: STAND has no movement window, and base pushboxes at x = -2 / +2
+// neither overlap each other nor the stage edges.
+__device__ __forceinline__ void intro_tick_fighter(Fighter& f, uint32_t in) {
+  f.hist = in & 3;
+  f.hold = (in & IN_ATTACK) ? 1 : 0;
+  const bool stunned = f.stun > 0;
+  f.stun -= stunned ? 1 : 0;
+  f.frame = stunned ? 0 : 1;
+}
+
+// Stop tick -> Intro (SetupBattleStart, bot Reset), Intro tick with the stale
+// actor inputs, -> Fight (frameCount = -1) and the state(-1) emission with the
+// bot's request (BC:178-200, 262-291, 329-345)
 template <int FM, bool BOT>
 __device__ __forceinline__ void stop_intro_fight(Arena& A) {
-  setup_battle_start(A.f[0], kP1StartX);
-  setup_battle_start(A.f[1], kP2StartX);
+  setup_battle_start(A.f0, kP1StartX);
+  setup_battle_start(A.f1, kP2StartX);
   if constexpr (BOT) bot_reset<FM>(A);
   record_input(A, A.act1, A.act2);
-  update_input(A.f[0], A.act1, 0);
-  update_input(A.f[1], A.act2, 1);
-  increment_action_frame(A.f[0]);
-  increment_action_frame(A.f[1]);
-  request_action(A.f[0], A_STAND);  // UpdateIntroAction (F:193-196)
-  request_action(A.f[1], A_STAND);
-  physics_tail<FM>(A);
+  intro_tick_fighter(A.f0, A.act1);
+  intro_tick_fighter(A.f1, A.act2);
   A.frame_count = -1;
   A.rec_count = 0;
   if constexpr (BOT) A.act2 = bot_next_input<FM>(A);
@@ -703,22 +759,20 @@ __device__ __forceinline__ void stop_intro_fight(Arena& A) {
 __device__ __forceinline__ void write_obs(const Arena& A, uint8_t* guard, uint8_t* move, float* move_frame,
                                           float* position, int32_t* frame, uint8_t* action, uint8_t* hitstun,
                                           size_t r) {
-  int m[2], mf[2];
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    int a = A.f[k].act;
-    if (a == A_DEAD || a == A_WIN) a = A_STAND;  // FE:537-549
-    m[k] = a;
-    mf[k] = (a == A_STAND || a == A_FORWARD || a == A_BACKWARD) ? 0 : A.f[k].frame;  // FE:339-358
-  }
+  int a0 = A.f0.act, a1 = A.f1.act;
+  if (a0 == A_DEAD || a0 == A_WIN) a0 = A_STAND;  // FE:537-549
+  if (a1 == A_DEAD || a1 == A_WIN) a1 = A_STAND;
+  const int m[2] = {a0, a1};
+  const int mf[2] = {(a0 == A_STAND || a0 == A_FORWARD || a0 == A_BACKWARD) ? 0 : A.f0.frame,  // FE:339-358
+                     (a1 == A_STAND || a1 == A_FORWARD || a1 == A_BACKWARD) ? 0 : A.f1.frame};
   const bool rec = A.rec_count > 0;
-  reinterpret_cast<uchar2*>(guard)[r] = make_uchar2((uint8_t)A.f[0].guard, (uint8_t)A.f[1].guard);
+  reinterpret_cast<uchar2*>(guard)[r] = make_uchar2((uint8_t)A.f0.guard, (uint8_t)A.f1.guard);
   reinterpret_cast<uchar2*>(move)[r] = make_uchar2((uint8_t)m[0], (uint8_t)m[1]);
   reinterpret_cast<float2*>(move_frame)[r] = make_float2((float)mf[0], (float)mf[1]);
-  reinterpret_cast<float2*>(position)[r] = make_float2(A.f[0].x, A.f[1].x);
+  reinterpret_cast<float2*>(position)[r] = make_float2(A.f0.x, A.f1.x);
   frame[r] = A.frame_count;
   reinterpret_cast<uchar2*>(action)[r] = make_uchar2(rec ? (uint8_t)A.rec1 : 0, rec ? (uint8_t)A.rec2 : 0);
-  reinterpret_cast<uchar2*>(hitstun)[r] = make_uchar2((uint8_t)A.f[0].stun, (uint8_t)A.f[1].stun);
+  reinterpret_cast<uchar2*>(hitstun)[r] = make_uchar2((uint8_t)A.f0.stun, (uint8_t)A.f1.stun);
 }
 
 __device__ __forceinline__ void write_main(const Arena& A, const DevOutputs& o, size_t r) {
@@ -747,7 +801,7 @@ __device__ __forceinline__ void env_step(Arena& A, uint32_t a1, uint32_t a2, con
   constexpr bool BOT = P2 == FS_P2_BOT;
   const DevOutputs& o = p.out;
   if (A.pending) {  // FS_AUTORESET_NEXT_STEP: this step runs the reset burst only
-    ko_and_end_ticks<FM>(A);
+    ko_and_end_ticks(A);
     stop_intro_fight<FM, BOT>(A);
     A.pending = false;
     A.has_term = false;
@@ -761,23 +815,23 @@ __device__ __forceinline__ void env_step(Arena& A, uint32_t a1, uint32_t a2, con
   A.act1 = a1;
   if constexpr (P2 == FS_P2_EXTERNAL) A.act2 = a2;
   else if constexpr (P2 == FS_P2_NOOP) A.act2 = 0;
-  const int g1 = A.f[0].guard, g2 = A.f[1].guard;  // guards of FE._current_state
+  const int g1 = A.f0.guard, g2 = A.f1.guard;  // guards of FE._current_state
   const bool over = fight_tick<FM>(A);
   double reward;
   if (p.dense_reward) {  // FE:388-405
     reward = 0.0;
-    if (A.f[0].guard < g1) reward -= 0.3;
-    if (A.f[1].guard < g2) reward += 0.3;
+    if (A.f0.guard < g1) reward -= 0.3;
+    if (A.f1.guard < g2) reward += 0.3;
     A.cum += reward;
-    if (over) reward += (double)(A.f[1].vital == 0 ? 1 : -1) - A.cum;
+    if (over) reward += (double)(A.f1.vital == 0 ? 1 : -1) - A.cum;
   } else {  // FE:382-386
-    reward = over ? (A.f[1].vital == 0 ? 1.0 : -1.0) : 0.0;
+    reward = over ? (A.f1.vital == 0 ? 1.0 : -1.0) : 0.0;
   }
   if (over) {
     ko_clear_input(A);
     if (p.autoreset_mode == FS_AUTORESET_SAME_STEP) {
       write_final(A, o, r);
-      ko_and_end_ticks<FM>(A);
+      ko_and_end_ticks(A);
       stop_intro_fight<FM, BOT>(A);
       A.cum = 0.0;
       A.has_term = false;
@@ -798,6 +852,7 @@ __device__ __forceinline__ void env_step(Arena& A, uint32_t a1, uint32_t a2, con
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step(StepParams p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  stage_tables();
   if (i >= p.n_envs) return;
   constexpr bool BOT = P2 == FS_P2_BOT;
   Arena A;
@@ -818,13 +873,14 @@ __global__ __launch_bounds__(256) void k_step(StepParams p) {
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  stage_tables();
   if (i >= p.n_envs) return;
   if (!p.init && p.mask && !p.mask[i]) return;
   constexpr bool BOT = P2 == FS_P2_BOT;
   Arena A;
   if (p.init) {  // `new Fighter()` defaults (F:73-112), round state Stop
     for (int k = 0; k < 2; k++) {
-      Fighter& f = A.f[k];
+      Fighter& f = k == 0 ? A.f0 : A.f1;
       f.x = 0.0f;
       f.hist = 0;
       f.act = A_STAND;
@@ -846,7 +902,7 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
   if (p.seeds) A.rng = rng_init((int32_t)(uint32_t)p.seeds[i]);  // SEED (BC:170-173)
   const bool hard = p.init || p.flags == FS_RESET_HARD || !A.has_term;
   if (A.pending) {  // finish the burst Unity ran after the terminal frame
-    ko_and_end_ticks<FM>(A);
+    ko_and_end_ticks(A);
     stop_intro_fight<FM, BOT>(A);
     A.pending = false;
   }
@@ -860,6 +916,16 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
   store_arena<BOT>(A, p.st, i);
 }
 
+// synthetic action stream (fs_hash_actions), one thread per (step, arena)
+__global__ __launch_bounds__(256) void k_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0,
+                                                       uint8_t* p1, uint8_t* p2) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)n_envs * n_steps) return;
+  const uint64_t env = idx % (size_t)n_envs, k = idx / (size_t)n_envs;
+  p1[idx] = (uint8_t)hash_action(seed, env, t0 + k, 0);
+  if (p2) p2[idx] = (uint8_t)hash_action(seed, env, t0 + k, 1);
+}
+
 // canonical export (fs_get_state / fs_get_env_state)
 template <bool BOT>
 __global__ __launch_bounds__(256) void k_get_state(DevState st, fs_arena_state* dst, fs_env_state* env, int n) {
@@ -870,7 +936,7 @@ __global__ __launch_bounds__(256) void k_get_state(DevState st, fs_arena_state* 
   if (dst) {
     fs_arena_state s;
     for (int k = 0; k < 2; k++) {
-      const Fighter& f = A.f[k];
+      const Fighter& f = k == 0 ? A.f0 : A.f1;
       fs_fighter_state& g = s.f[k];
       g.position_x = f.x;
       g.action_id = kActionId[f.act];
@@ -920,21 +986,21 @@ __global__ __launch_bounds__(256) void k_get_state(DevState st, fs_arena_state* 
   }
   if (env) {
     fs_env_state e;
-    e.p1Vital = A.f[0].vital;
-    e.p2Vital = A.f[1].vital;
-    e.p1Guard = A.f[0].guard;
-    e.p2Guard = A.f[1].guard;
-    e.p1Move = kActionId[A.f[0].act];
-    e.p1MoveFrame = A.f[0].frame;
-    e.p2Move = kActionId[A.f[1].act];
-    e.p2MoveFrame = A.f[1].frame;
-    e.p1Position = A.f[0].x;
-    e.p2Position = A.f[1].x;
+    e.p1Vital = A.f0.vital;
+    e.p2Vital = A.f1.vital;
+    e.p1Guard = A.f0.guard;
+    e.p2Guard = A.f1.guard;
+    e.p1Move = kActionId[A.f0.act];
+    e.p1MoveFrame = A.f0.frame;
+    e.p2Move = kActionId[A.f1.act];
+    e.p2MoveFrame = A.f1.frame;
+    e.p1Position = A.f0.x;
+    e.p2Position = A.f1.x;
     e.globalFrame = A.frame_count;
     e.p1MostRecentAction = A.rec_count > 0 ? (int32_t)A.rec1 : 0;
     e.p2MostRecentAction = A.rec_count > 0 ? (int32_t)A.rec2 : 0;
-    e.p1Hitstun = A.f[0].stun;
-    e.p2Hitstun = A.f[1].stun;
+    e.p1Hitstun = A.f0.stun;
+    e.p2Hitstun = A.f1.stun;
     env[i] = e;
   }
 }
@@ -953,7 +1019,7 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
   Arena A;
   for (int k = 0; k < 2; k++) {
     const fs_fighter_state& g = s.f[k];
-    Fighter& f = A.f[k];
+    Fighter& f = k == 0 ? A.f0 : A.f1;
     f.x = g.position_x;
     f.act = action_index_of(g.action_id);
     f.frame = g.action_frame;
@@ -1024,6 +1090,14 @@ static hipError_t launch_reset_fm(const ResetParams& p, int p2_mode, hipStream_t
 hipError_t launch_reset(const ResetParams& p, int float_mode, int p2_mode, hipStream_t s) {
   return float_mode == FS_FLOAT_DOUBLE ? launch_reset_fm<FS_FLOAT_DOUBLE>(p, p2_mode, s)
                                        : launch_reset_fm<FS_FLOAT_STRICT32>(p, p2_mode, s);
+}
+
+hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1, uint8_t* p2,
+                               hipStream_t s) {
+  const size_t total = (size_t)n_envs * n_steps;
+  hipLaunchKernelGGL(k_hash_actions, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n_envs,
+                     n_steps, seed, t0, p1, p2);
+  return hipGetLastError();
 }
 
 hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_state* env, int n, int p2_mode,

@@ -147,6 +147,15 @@ class FootsiesSim:
                               None if t is None else C.byref(t)), self._h)
         return trajectory if trajectory is not None else self._out
 
+    def hash_actions(self, n_steps, seed=0x5EED, t0=0, p2=True):
+        """Device uint8 [n_steps][N] action arrays from the synthetic splitmix64 stream."""
+        torch = _torch()
+        p1 = torch.empty((n_steps, self.num_envs), dtype=torch.uint8, device=self.device)
+        q2 = torch.empty((n_steps, self.num_envs), dtype=torch.uint8, device=self.device) if p2 else None
+        check(lib().fs_hash_actions(self._h, int(n_steps), int(seed), int(t0), C.c_void_p(p1.data_ptr()),
+                                    C.c_void_p(q2.data_ptr()) if p2 else None), self._h)
+        return p1, q2
+
     def alloc_trajectory(self, n):
         torch = _torch()
         out = {}

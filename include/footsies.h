@@ -192,6 +192,12 @@ int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags
 int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act,
               uint64_t action_seed, const fs_outputs* traj);
 
+/* Fill device arrays p1_out/p2_out [n_steps][N] with the synthetic action stream
+ * of fs_step_n (splitmix64 hash of (seed, env, t0 + k, player)),
+ * so benchmark inputs are resident in HBM before the timed region.
+ * p2_out may be NULL. */
+int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out);
+
 /* Device pointers of the current outputs, valid until the next call on h. */
 int fs_outputs_get(fs_handle h, fs_outputs* out);
 
