@@ -37,29 +37,29 @@ constexpr uint32_t IN_LEFT = 1, IN_RIGHT = 2, IN_ATTACK = 4;
 // LDS it costs ~tens of cycles instead of an L1/L2 round trip.  ~4.3 KB per
 // block, copied once per launch by all threads of the block.
 // ---------------------------------------------------------------------------
-struct Tables {
-  ActionInfo action[kNumActions];
-  uint32_t rows[kNumRows];
-  float4 rects[kNumRects];
-  float vels[kNumVels];
-  uint32_t hitsets[kNumHitSets];
-  uint32_t hurtsets[kNumHurtSets];
-  uint32_t cancel[kNumCancelMasks];
-  AttackInfo attacks[4];
-};
 __shared__ Tables sT;
 
-// all threads of the block must call this before any early return
+// Copy the kTables image (fs_tables.h) into LDS: every thread issues all of its
+// loads before any store, so the block waits for one round trip, not one per table.
+// All threads of the block must call this before any early return.
+constexpr int kBlock = 256;
 __device__ __forceinline__ void stage_tables() {
-  const int t = threadIdx.x, nt = blockDim.x;
-  for (int i = t; i < kNumRows; i += nt) sT.rows[i] = kRows[i];
-  for (int i = t; i < kNumActions; i += nt) sT.action[i] = kActionInfo[i];
-  for (int i = t; i < kNumRects; i += nt) sT.rects[i] = kRects[i];
-  for (int i = t; i < kNumVels; i += nt) sT.vels[i] = kVels[i];
-  for (int i = t; i < kNumHitSets; i += nt) sT.hitsets[i] = kHitSets[i];
-  for (int i = t; i < kNumHurtSets; i += nt) sT.hurtsets[i] = kHurtSets[i];
-  for (int i = t; i < kNumCancelMasks; i += nt) sT.cancel[i] = kCancelMasks[i];
-  for (int i = t; i < 4; i += nt) sT.attacks[i] = kAttacks[i];
+  constexpr int kWords = sizeof(Tables) / 4;
+  constexpr int kPer = (kWords + kBlock - 1) / kBlock;
+  static_assert(sizeof(Tables) % 4 == 0, "table image must be word-sized");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&kTables);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&sT);
+  uint32_t v[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int i = threadIdx.x + j * kBlock;
+    v[j] = i < kWords ? src[i] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int i = threadIdx.x + j * kBlock;
+    if (i < kWords) dst[i] = v[j];
+  }
   __syncthreads();
 }
 
@@ -470,45 +470,42 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
   return DR_DAMAGE;
 }
 
-// one attacker of UpdateHitboxHurtboxCollision (BC:521-591)
+// The box test of one attacker of UpdateHitboxHurtboxCollision (BC:535-569):
+// attacker hitboxes in order, skipping attacks that already hit (CanAttackHit,
+// F:408-420); a proximity box only flags proximity, a real box is a hit and ends
+// the scan.
+struct HitTest {
+  bool hit, prox;
+  int atk;
+};
+
 template <int FM>
-__device__ __forceinline__ void collide(Fighter& att, Fighter& def) {
-  const int nh = att.hitset & 3;
-  if (nh == 0) return;  // only attack actions carry hitboxes
-  const int nu = def.hurtset & 3;
-  bool hit = false, prox = false;
-  int atk = 0;
+__device__ __forceinline__ HitTest hit_test(uint32_t hitset, float hx0, float hx1, int hits, uint32_t hurtset,
+                                            float ux0, float ux1) {
+  HitTest t{false, false, 0};
+  const int nh = hitset & 3, nu = hurtset & 3;
   for (int h = 0; h < nh; h++) {
-    const uint32_t hb = (att.hitset >> (2 + 9 * h)) & 511;
+    const uint32_t hb = (hitset >> (2 + 9 * h)) & 511;
     const int aidx = (hb >> 6) & 3;
-    if (att.hits >= sT.attacks[aidx].number_of_hit) continue;  // CanAttackHit (F:408-420)
+    if (hits >= sT.attacks[aidx].number_of_hit) continue;
     const float4 hr = sT.rects[hb & 63];
-    const float hx = h == 0 ? att.hx0 : att.hx1;
+    const float hx = h == 0 ? hx0 : hx1;
     for (int u = 0; u < nu; u++) {
-      const float4 ur = sT.rects[(def.hurtset >> (2 + 6 * u)) & 63];
-      const float ux = u == 0 ? def.ux0 : def.ux1;
+      const float4 ur = sT.rects[(hurtset >> (2 + 6 * u)) & 63];
+      const float ux = u == 0 ? ux0 : ux1;
       if (box_overlaps<FM>(hx, hr, ux, ur)) {
         if ((hb >> 8) & 1) {
-          prox = true;
+          t.prox = true;
         } else {
-          hit = true;
-          atk = aidx;
+          t.hit = true;
+          t.atk = aidx;
           break;
         }
       }
     }
-    if (hit) break;
+    if (t.hit) break;
   }
-  if (hit) {
-    att.hits++;  // NotifyAttackHit (F:352-355)
-    const AttackInfo ad = sT.attacks[atk];
-    const int res = notify_damaged(def, ad);
-    const int stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
-    att.stun = stun;  // SetHitStun on both (BC:576-578)
-    def.stun = stun;
-  } else if (prox) {
-    if (def.in_back) def.prox = true;  // NotifyInProximityGuardRange (F:400-406)
-  }
+  return t;
 }
 
 // ---------------------------------------------------------------------------
@@ -609,88 +606,201 @@ __device__ __forceinline__ uint32_t select_attack(uint4& rng, float d, uint32_t 
   return rng_range(rng, 0, 3) == 0 ? AP_ONE_HIT : AP_TWO_HIT;
 }
 
+// getNextAIInput (AI:41-66) for the P2 bot.  The ascending copy loop of
+// UpdateFightState (AI:358-361) leaves fightStates[5] == the *previous* call's
+// state, so the bot keeps one FightState: (distance, opponent action).
+struct Bot {
+  uint4 rng;
+  uint32_t mplan, midx, aplan, aidx, prev_opp;
+  float prev_dist;
+};
+
+// Mathf.Abs(fighter2.x - fighter1.x) (AI:370-373)
 template <int FM>
-__device__ __forceinline__ float bot_distance(const Arena& A) {  // Mathf.Abs(f2.x - f1.x) (AI:370-373)
-  return fabsf(fsub<FM>(A.f1.x, A.f0.x));
+__device__ __forceinline__ float bot_distance(float x1, float x2) {
+  return fabsf(fsub<FM>(x2, x1));
 }
 
-template <int FM>
-__device__ __forceinline__ void bot_reset(Arena& A) {  // AI:393-403
-  A.mplan = A.midx = A.aplan = A.aidx = 0;
-  A.prev_dist = bot_distance<FM>(A);
-  A.prev_opp = A.f0.act;
-}
-
-// getNextAIInput (AI:41-66).  The ascending copy loop of UpdateFightState
-// (AI:358-361) makes fightStates[5] the *previous* call's state.
-template <int FM>
-__device__ __forceinline__ uint32_t bot_next_input(Arena& A) {
-  const float d = A.prev_dist;
-  const uint32_t opp = A.prev_opp;
-  A.prev_dist = bot_distance<FM>(A);
-  A.prev_opp = A.f0.act;
+__device__ __forceinline__ uint32_t bot_next_input(Bot& b, float dist, uint32_t opp_act) {
+  const float d = b.prev_dist;
+  const uint32_t opp = b.prev_opp;
+  b.prev_dist = dist;
+  b.prev_opp = opp_act;
   uint32_t input = 0;
-  if (A.mplan) {
-    input |= move_plan_input(A.mplan - 1, A.midx);
-    if (++A.midx == move_plan_len(A.mplan - 1)) A.mplan = 0;
+  if (b.mplan) {
+    input |= move_plan_input(b.mplan - 1, b.midx);
+    if (++b.midx == move_plan_len(b.mplan - 1)) b.mplan = 0;
   } else {
-    A.mplan = select_movement(A.rng, d) + 1;
-    A.midx = 0;
+    b.mplan = select_movement(b.rng, d) + 1;
+    b.midx = 0;
   }
-  if (A.aplan) {
-    input |= attack_plan_input(A.aplan - 1, A.aidx);
-    if (++A.aidx == attack_plan_len(A.aplan - 1)) A.aplan = 0;
+  if (b.aplan) {
+    input |= attack_plan_input(b.aplan - 1, b.aidx);
+    if (++b.aidx == attack_plan_len(b.aplan - 1)) b.aplan = 0;
   } else {
-    A.aplan = select_attack(A.rng, d, opp) + 1;
-    A.aidx = 0;
+    b.aplan = select_attack(b.rng, d, opp) + 1;
+    b.aidx = 0;
   }
   return input;
 }
 
 // ---------------------------------------------------------------------------
-// round flow (BC:138-345)
+// Two lanes per arena.  Lane 2a+k runs fighter k of arena a (k = 0: P1, faces
+// right; k = 1: P2).  Per-fighter phases (UpdateInput .. UpdateBoxes) run on
+// both lanes at once; the pair phases (character push, hit/hurt collision, KO,
+// reward) exchange the partner's values with one DPP quad_perm [1,0,3,2] move
+// per 32-bit value.  Arena-level fields (frameCount, recording count, reward
+// accumulator, reset flags) are kept as identical replicas on both lanes and
+// stored by lane k = 0; the bot lives on the P2 lane.  Every exchange sits in
+// control flow that is uniform across a pair, so the partner lane is active.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void record_input(Arena& A, uint32_t p1, uint32_t p2) {  // BC:593-607
-  if (A.rec_count >= kMaxRecording) return;
-  A.rec1 = p1;
-  A.rec2 = p2;
-  A.rec_count++;
+__device__ __forceinline__ uint32_t xpair(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1 /* quad_perm(1,0,3,2) */, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int xpair(int v) { return (int)xpair((uint32_t)v); }
+__device__ __forceinline__ float xpair(float v) { return __uint_as_float(xpair(__float_as_uint(v))); }
+
+struct Lane {
+  Fighter f;
+  uint32_t k;         // 0: P1, 1: P2
+  int frame_count;    // replicas ...
+  uint32_t rec_count;
+  bool pending, has_term;
+  double cum;
+  uint32_t rec;       // this player's recordingPnInput[index - 1]
+  uint32_t act;       // this player's TrainingActor.GetInput()
+  Bot bot;            // P2 lane, FS_P2_BOT only
+};
+
+template <bool BOT>
+__device__ __forceinline__ void load_lane(Lane& L, const DevState& s, int a, uint32_t k) {
+  const int l = 2 * a + (int)k;
+  L.k = k;
+  L.f.x = reinterpret_cast<const float*>(s.pos)[l];
+  L.f.hist = reinterpret_cast<const uint32_t*>(s.hist)[l];
+  const uint2 w = reinterpret_cast<const uint2*>(s.fpk)[l];
+  const int2 aw = s.aw[a];
+  L.cum = s.cum[a];
+  unpack_fighter(L.f, w.x, w.y);
+  const uint32_t h = (uint32_t)aw.y;
+  L.frame_count = aw.x;
+  L.rec_count = h & 0x7fff;
+  L.rec = (h >> (k ? 18 : 15)) & 7;
+  L.act = (h >> (k ? 24 : 21)) & 7;
+  L.pending = (h >> 27) & 1;
+  L.has_term = (h >> 28) & 1;
+  if constexpr (BOT) {  // both lanes read the same 24 B (one cache line); P2 uses it
+    L.bot.rng = s.rng[a];
+    const uint2 b = s.bot[a];
+    L.bot.mplan = b.x & 7;
+    L.bot.midx = (b.x >> 3) & 127;
+    L.bot.aplan = (b.x >> 10) & 7;
+    L.bot.aidx = (b.x >> 13) & 127;
+    L.bot.prev_opp = (b.x >> 20) & 31;
+    L.bot.prev_dist = __uint_as_float(b.y);
+  }
 }
 
+template <bool BOT>
+__device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int a) {
+  const int l = 2 * a + (int)L.k;
+  const uint64_t w = pack_fighter(L.f);
+  reinterpret_cast<float*>(s.pos)[l] = L.f.x;
+  reinterpret_cast<uint32_t*>(s.hist)[l] = L.f.hist;
+  reinterpret_cast<uint2*>(s.fpk)[l] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+  const uint32_t other = xpair(L.rec | (L.act << 3));  // P2's recorded/actor input for the header
+  if (L.k == 0) {
+    const uint32_t h = L.rec_count | (L.rec << 15) | ((other & 7) << 18) | (L.act << 21) | ((other >> 3) << 24) |
+                       ((uint32_t)L.pending << 27) | ((uint32_t)L.has_term << 28);
+    s.aw[a] = make_int2(L.frame_count, (int)h);
+    s.cum[a] = L.cum;
+  }
+  if constexpr (BOT) {
+    if (L.k == 1) {
+      const Bot& b = L.bot;
+      s.rng[a] = b.rng;
+      s.bot[a] = make_uint2(b.mplan | (b.midx << 3) | (b.aplan << 10) | (b.aidx << 13) | (b.prev_opp << 20),
+                            __float_as_uint(b.prev_dist));
+    }
+  }
+}
+
+// UpdatePushCharacterVsCharacter (BC:483-501) with UnityEngine.Rect semantics:
+// x is xMin, xMax = width + x, Overlaps is strict.  Both lanes evaluate the same
+// expressions on (P1, P2) values; each applies its own fighter's shift.
 template <int FM>
-__device__ __forceinline__ void physics_tail(Arena& A) {  // movement, boxes, pushes (shared by all tick kinds)
-  update_movement<FM>(A.f0, 1.0f);
-  update_movement<FM>(A.f1, -1.0f);
-  update_boxes<FM>(A.f0, 1.0f);
-  update_boxes<FM>(A.f1, -1.0f);
-  push_character_vs_character<FM>(A.f0, A.f1);
-  push_character_vs_background<FM>(A.f0);
-  push_character_vs_background<FM>(A.f1);
+__device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t k) {
+  const float o_px = xpair(f.px), o_x = xpair(f.x);
+  const int o_rect = xpair(f.push_rect);
+  const float px1 = k == 0 ? f.px : o_px, px2 = k == 0 ? o_px : f.px;
+  const float x1 = k == 0 ? f.x : o_x, x2 = k == 0 ? o_x : f.x;
+  const float4 r1 = sT.rects[k == 0 ? f.push_rect : o_rect], r2 = sT.rects[k == 0 ? o_rect : f.push_rect];
+  const float xmax1 = fadd<FM>(r1.z, px1), xmax2 = fadd<FM>(r2.z, px2);
+  const float ymax1 = fadd<FM>(r1.w, r1.y), ymax2 = fadd<FM>(r2.w, r2.y);
+  const bool overlap = xmax2 > px1 && px2 < xmax1 && ymax2 > r1.y && r2.y < ymax1;
+  if (!overlap || x1 == x2) return;  // a tie pushes nothing (BC:490-499)
+  float d1, d2;  // shifts of P1, P2
+  if constexpr (FM == FS_FLOAT_DOUBLE) {
+    const double d = x1 < x2 ? (double)xmax1 - (double)px2 : (double)xmax2 - (double)px1;
+    d1 = x1 < x2 ? (float)(d * -1 / 2) : (float)(d * 1 / 2);
+    d2 = x1 < x2 ? (float)(d * 1 / 2) : (float)(d * -1 / 2);
+  } else {
+    const float d = x1 < x2 ? __fsub_rn(xmax1, px2) : __fsub_rn(xmax2, px1);
+    d1 = x1 < x2 ? d * -1.0f / 2.0f : d * 1.0f / 2.0f;
+    d2 = x1 < x2 ? d * 1.0f / 2.0f : d * -1.0f / 2.0f;
+  }
+  apply_position_change<FM>(f, k == 0 ? d1 : d2);
 }
 
-// UpdateFightState (BC:347-364); returns battleOver (BC:212-213)
+// UpdateHitboxHurtboxCollision (BC:521-591): attacker P1 then attacker P2.  The
+// boxes are those of UpdateBoxes (not rebuilt when a hit changes the action), but
+// the hit count is re-read: P2's may have been reset by P1's hit (sequential trade
+// semantics).  Both lanes run the same box test; the defender lane applies
+// NotifyDamaged, the attacker lane NotifyAttackHit, and both take the stun.
 template <int FM>
-__device__ __forceinline__ bool fight_tick(Arena& A) {
-  A.frame_count++;
-  record_input(A, A.act1, A.act2);
-  const InputEval e0 = update_input(A.f0, A.act1, 0);
-  const InputEval e1 = update_input(A.f1, A.act2, 1);
-  increment_action_frame(A.f0);
-  increment_action_frame(A.f1);
-  update_action_request(A.f0, e0);
-  update_action_request(A.f1, e1);
-  physics_tail<FM>(A);
-  collide<FM>(A.f0, A.f1);
-  collide<FM>(A.f1, A.f0);
-  return A.f0.vital <= 0 || A.f1.vital <= 0;
+__device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k) {
+  const uint32_t o_hitset = xpair(f.hitset), o_hurtset = xpair(f.hurtset);
+  const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1), o_ux0 = xpair(f.ux0), o_ux1 = xpair(f.ux1);
+  if (((f.hitset | o_hitset) & 3) == 0) return;  // only attack actions carry hitboxes
+#pragma unroll
+  for (uint32_t phase = 0; phase < 2; phase++) {
+    const bool attacking = k == phase;
+    const int o_hits = xpair(f.hits);
+    const HitTest t = attacking ? hit_test<FM>(f.hitset, f.hx0, f.hx1, f.hits, o_hurtset, o_ux0, o_ux1)
+                                : hit_test<FM>(o_hitset, o_hx0, o_hx1, o_hits, f.hurtset, f.ux0, f.ux1);
+    int stun = 0;
+    if (t.hit) {
+      const AttackInfo ad = sT.attacks[t.atk];
+      if (attacking) {
+        f.hits++;  // NotifyAttackHit (F:352-355)
+      } else {
+        const int res = notify_damaged(f, ad);
+        stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
+      }
+    }
+    const int o_stun = xpair(stun);
+    if (t.hit) f.stun = attacking ? o_stun : stun;  // SetHitStun on both (BC:576-578)
+    else if (t.prox && !attacking && f.in_back) f.prox = true;  // NotifyInProximityGuardRange (F:400-406)
+  }
 }
 
-__device__ __forceinline__ void ko_clear_input(Arena& A) {  // ChangeRoundState(KO): ClearInput (BC:292-299)
-  A.f0.hist = A.f1.hist = 0;
-  A.f0.hold = A.f1.hold = 0;
+// KO tick -> End (winner), End tick (BC:221-243, 306-325, 371-381), reduced to
+// its observable effects.  SetupBattleStart (next tick) overwrites position,
+// action, frame, hit count, buffer, reserve, vital, guard, hasWon and the input
+// history, so what survives the End tick is (a) the hitstun decrement and (b)
+// UpdateActionRequest clearing isInputBackward / isReserveProximityGuard --
+// unless it returned early: for the winner (hasWon), or on the reserve / buffer
+// paths (F:204-229).  The history was cleared at KO, so the fall-through sees no input.
+__device__ __forceinline__ void end_tick(Fighter& f, bool won) {
+  f.stun -= f.stun > 0 ? 1 : 0;
+  const bool early = won || (f.rsv != NONE && f.stun <= 0) ||
+                     (f.buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0);
+  f.in_back = early ? f.in_back : false;
+  f.prox = early ? f.prox : false;
 }
 
-__device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {  // F:120-135
+// SetupBattleStart (F:120-135): hitstun and the two guard latches are NOT reset
+__device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {
   f.x = x;
   f.vital = 1;
   f.guard = kStartGuard;
@@ -700,86 +810,72 @@ __device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {  // F:
   set_action(f, A_STAND);
 }
 
-// KO tick -> End (winner), End tick (BC:221-243, 306-325, 371-381), reduced to
-// its observable effects.  The End tick runs IncrementActionFrame,
-// UpdateActionRequest, movement, boxes and pushes, but SetupBattleStart (next
-// tick) overwrites position, action, frame, hit count, buffer, reserve, vital,
-// guard, hasWon and the input history.  What survives is (a) the hitstun
-// decrement and (b) UpdateActionRequest clearing isInputBackward /
-// isReserveProximityGuard -- which it does unless it returned early: for the
-// winner (hasWon), or on the reserve / buffer paths (F:204-229).  The input
-// history was cleared at KO, so the fall-through path sees no input.
-__device__ __forceinline__ void end_tick_effects(Fighter& f, bool won) {
-  const bool stunned = f.stun > 0;
-  f.stun -= stunned ? 1 : 0;  // IncrementActionFrame (F:150-154); the frame itself is overwritten
-  const bool early = won || (f.rsv != NONE && f.stun <= 0) ||
-                     (f.buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0);
-  f.in_back = early ? f.in_back : false;
-  f.prox = early ? f.prox : false;
-}
-
-__device__ __forceinline__ void ko_and_end_ticks(Arena& A) {
-  const bool d0 = A.f0.vital <= 0, d1 = A.f1.vital <= 0;
-  end_tick_effects(A.f0, A.f0.won || (d1 && !d0));  // a sole survivor gets RequestWinAction (BC:310-323)
-  end_tick_effects(A.f1, A.f1.won || (d0 && !d1));
-}
-
-// Intro tick for one fighter right after SetupBattleStart (BC:329-345): the stale
-// actor input enters the cleared history, the frame advances unless in hitstun,
-// and RequestAction(STAND) on STAND is a no-op.  Movement, boxes and both pushes
-// are no-ops here: STAND has no movement window, and base pushboxes at x = -2 / +2
-// neither overlap each other nor the stage edges.
-__device__ __forceinline__ void intro_tick_fighter(Fighter& f, uint32_t in) {
-  f.hist = in & 3;
-  f.hold = (in & IN_ATTACK) ? 1 : 0;
-  const bool stunned = f.stun > 0;
-  f.stun -= stunned ? 1 : 0;
-  f.frame = stunned ? 0 : 1;
-}
-
-// Stop tick -> Intro (SetupBattleStart, bot Reset), Intro tick with the stale
-// actor inputs, -> Fight (frameCount = -1) and the state(-1) emission with the
-// bot's request (BC:178-200, 262-291, 329-345)
+// The reset burst of one lane (BC:212-345).  after_ko: the KO -> End -> Stop ->
+// Intro -> Fight sequence after a terminal frame (ClearInput already applied);
+// otherwise the RESET / game-start path Stop -> Intro -> Fight.
+//   Intro tick: the stale actor input enters the cleared history, the frame
+//   advances unless in hitstun, RequestAction(STAND) on STAND is a no-op, and
+//   movement / boxes / pushes are no-ops (STAND has no movement window; base
+//   pushboxes at x = -2 / +2 neither overlap nor touch the stage edges).
+//   Fight: frameCount = -1, recording index 0, state(-1) emitted, and the bot's
+//   first RequestNextInput.
 template <int FM, bool BOT>
-__device__ __forceinline__ void stop_intro_fight(Arena& A) {
-  setup_battle_start(A.f0, kP1StartX);
-  setup_battle_start(A.f1, kP2StartX);
-  if constexpr (BOT) bot_reset<FM>(A);
-  record_input(A, A.act1, A.act2);
-  intro_tick_fighter(A.f0, A.act1);
-  intro_tick_fighter(A.f1, A.act2);
-  A.frame_count = -1;
-  A.rec_count = 0;
-  if constexpr (BOT) A.act2 = bot_next_input<FM>(A);
+__device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
+  if (after_ko) {
+    const int o_vital = xpair(L.f.vital);
+    end_tick(L.f, L.f.won || (L.f.vital > 0 && o_vital <= 0));  // a sole survivor wins (BC:310-323)
+  }
+  setup_battle_start(L.f, L.k == 0 ? kP1StartX : kP2StartX);
+  const float o_x = xpair(L.f.x);
+  const uint32_t o_act = xpair((uint32_t)L.f.act);
+  const float x1 = L.k == 0 ? L.f.x : o_x, x2 = L.k == 0 ? o_x : L.f.x;
+  const uint32_t p1_act = L.k == 0 ? (uint32_t)L.f.act : o_act;
+  if constexpr (BOT) {  // BattleAI.Reset (AI:393-403)
+    L.bot.mplan = L.bot.midx = L.bot.aplan = L.bot.aidx = 0;
+    L.bot.prev_dist = bot_distance<FM>(x1, x2);
+    L.bot.prev_opp = p1_act;
+  }
+  if (L.rec_count < kMaxRecording) {  // RecordInput in the Intro tick (BC:333)
+    L.rec = L.act;
+    L.rec_count++;
+  }
+  L.f.hist = L.act & 3;
+  L.f.hold = (L.act & IN_ATTACK) ? 1 : 0;
+  const bool stunned = L.f.stun > 0;
+  L.f.stun -= stunned ? 1 : 0;
+  L.f.frame = stunned ? 0 : 1;
+  L.frame_count = -1;
+  L.rec_count = 0;
+  if constexpr (BOT) {
+    if (L.k == 1) L.act = bot_next_input(L.bot, bot_distance<FM>(x1, x2), p1_act);
+  }
 }
 
 // ---------------------------------------------------------------------------
-// outputs (FE:336-380, 537-549)
+// outputs (FE:336-380, 537-549): each lane writes its own column of the [N][2]
+// pairs (one byte / float per lane, fully coalesced); lane k = 0 the per-arena ones
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void write_obs(const Arena& A, uint8_t* guard, uint8_t* move, float* move_frame,
+__device__ __forceinline__ void write_obs(const Lane& L, uint8_t* guard, uint8_t* move, float* move_frame,
                                           float* position, int32_t* frame, uint8_t* action, uint8_t* hitstun,
                                           size_t r) {
-  int a0 = A.f0.act, a1 = A.f1.act;
-  if (a0 == A_DEAD || a0 == A_WIN) a0 = A_STAND;  // FE:537-549
-  if (a1 == A_DEAD || a1 == A_WIN) a1 = A_STAND;
-  const int m[2] = {a0, a1};
-  const int mf[2] = {(a0 == A_STAND || a0 == A_FORWARD || a0 == A_BACKWARD) ? 0 : A.f0.frame,  // FE:339-358
-                     (a1 == A_STAND || a1 == A_FORWARD || a1 == A_BACKWARD) ? 0 : A.f1.frame};
-  const bool rec = A.rec_count > 0;
-  reinterpret_cast<uchar2*>(guard)[r] = make_uchar2((uint8_t)A.f0.guard, (uint8_t)A.f1.guard);
-  reinterpret_cast<uchar2*>(move)[r] = make_uchar2((uint8_t)m[0], (uint8_t)m[1]);
-  reinterpret_cast<float2*>(move_frame)[r] = make_float2((float)mf[0], (float)mf[1]);
-  reinterpret_cast<float2*>(position)[r] = make_float2(A.f0.x, A.f1.x);
-  frame[r] = A.frame_count;
-  reinterpret_cast<uchar2*>(action)[r] = make_uchar2(rec ? (uint8_t)A.rec1 : 0, rec ? (uint8_t)A.rec2 : 0);
-  reinterpret_cast<uchar2*>(hitstun)[r] = make_uchar2((uint8_t)A.f0.stun, (uint8_t)A.f1.stun);
+  int a = L.f.act;
+  if (a == A_DEAD || a == A_WIN) a = A_STAND;  // FE:537-549
+  const int mf = (a == A_STAND || a == A_FORWARD || a == A_BACKWARD) ? 0 : L.f.frame;  // FE:339-358
+  const size_t c = 2 * r + L.k;
+  guard[c] = (uint8_t)L.f.guard;
+  move[c] = (uint8_t)a;
+  move_frame[c] = (float)mf;
+  position[c] = L.f.x;
+  action[c] = L.rec_count > 0 ? (uint8_t)L.rec : 0;
+  hitstun[c] = (uint8_t)L.f.stun;
+  if (L.k == 0) frame[r] = L.frame_count;
 }
 
-__device__ __forceinline__ void write_main(const Arena& A, const DevOutputs& o, size_t r) {
-  write_obs(A, o.guard, o.move, o.move_frame, o.position, o.frame, o.action, o.hitstun, r);
+__device__ __forceinline__ void write_main(const Lane& L, const DevOutputs& o, size_t r) {
+  write_obs(L, o.guard, o.move, o.move_frame, o.position, o.frame, o.action, o.hitstun, r);
 }
-__device__ __forceinline__ void write_final(const Arena& A, const DevOutputs& o, size_t r) {
-  write_obs(A, o.final_guard, o.final_move, o.final_move_frame, o.final_position, o.final_frame, o.final_action,
+__device__ __forceinline__ void write_final(const Lane& L, const DevOutputs& o, size_t r) {
+  write_obs(L, o.final_guard, o.final_move, o.final_move_frame, o.final_position, o.final_frame, o.final_action,
             o.final_hitstun, r);
 }
 
@@ -794,126 +890,163 @@ __device__ __forceinline__ uint32_t hash_action(uint64_t seed, uint64_t env, uin
 }
 
 // ---------------------------------------------------------------------------
-// one env-step of one arena: FootsiesEnv.step (FE:518-570) over the synced game
+// one env-step: FootsiesEnv.step (FE:518-570) over the synced game's Fight tick
+// (BC:201-220, 347-364) and, for a terminal arena, the auto-reset burst
 // ---------------------------------------------------------------------------
 template <int FM, int P2>
-__device__ __forceinline__ void env_step(Arena& A, uint32_t a1, uint32_t a2, const StepParams& p, size_t r) {
+__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, size_t r) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   const DevOutputs& o = p.out;
-  if (A.pending) {  // FS_AUTORESET_NEXT_STEP: this step runs the reset burst only
-    ko_and_end_ticks(A);
-    stop_intro_fight<FM, BOT>(A);
-    A.pending = false;
-    A.has_term = false;
-    A.cum = 0.0;
-    write_main(A, o, r);
-    o.reward[r] = 0.0;
-    o.terminated[r] = 0;
-    o.truncated[r] = 0;
+  const uint32_t k = L.k;
+  if (L.pending) {  // FS_AUTORESET_NEXT_STEP: this step runs the reset burst only
+    reset_burst<FM, BOT>(L, true);
+    L.pending = false;
+    L.has_term = false;
+    L.cum = 0.0;
+    write_main(L, o, r);
+    if (k == 0) {
+      o.reward[r] = 0.0;
+      o.terminated[r] = 0;
+      o.truncated[r] = 0;
+    }
     return;
   }
-  A.act1 = a1;
-  if constexpr (P2 == FS_P2_EXTERNAL) A.act2 = a2;
-  else if constexpr (P2 == FS_P2_NOOP) A.act2 = 0;
-  const int g1 = A.f0.guard, g2 = A.f1.guard;  // guards of FE._current_state
-  const bool over = fight_tick<FM>(A);
+  // the actor inputs of this frame (TrainingManager.p1Input/p2Input, BC:383-447)
+  if (k == 0 || P2 == FS_P2_EXTERNAL) L.act = a_own;
+  else if (P2 == FS_P2_NOOP) L.act = 0;  // FS_P2_BOT: the input the bot computed after the last frame
+  const int guard_before = L.f.guard;  // guards of FE._current_state
+  L.frame_count++;
+  if (L.rec_count < kMaxRecording) {  // RecordInput (BC:593-607)
+    L.rec = L.act;
+    L.rec_count++;
+  }
+  const float sign = k == 0 ? 1.0f : -1.0f;
+  const InputEval e = update_input(L.f, L.act, (int)k);
+  increment_action_frame(L.f);
+  update_action_request(L.f, e);
+  update_movement<FM>(L.f, sign);
+  update_boxes<FM>(L.f, sign);
+  push_character_vs_character<FM>(L.f, k);
+  push_character_vs_background<FM>(L.f);
+  hitbox_hurtbox_collision<FM>(L.f, k);
+  // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes
+  const uint32_t mine = (uint32_t)L.f.vital | ((uint32_t)L.f.guard << 2) | ((uint32_t)guard_before << 4);
+  const uint32_t theirs = xpair(mine);
+  const uint32_t w1 = k == 0 ? mine : theirs, w2 = k == 0 ? theirs : mine;
+  const int v1 = w1 & 3, v2 = w2 & 3;
+  const bool over = v1 <= 0 || v2 <= 0;
   double reward;
-  if (p.dense_reward) {  // FE:388-405
+  if (p.dense_reward) {
     reward = 0.0;
-    if (A.f0.guard < g1) reward -= 0.3;
-    if (A.f1.guard < g2) reward += 0.3;
-    A.cum += reward;
-    if (over) reward += (double)(A.f1.vital == 0 ? 1 : -1) - A.cum;
-  } else {  // FE:382-386
-    reward = over ? (A.f1.vital == 0 ? 1.0 : -1.0) : 0.0;
+    if (((w1 >> 2) & 3) < (w1 >> 4)) reward -= 0.3;
+    if (((w2 >> 2) & 3) < (w2 >> 4)) reward += 0.3;
+    L.cum += reward;
+    if (over) reward += (double)(v2 == 0 ? 1 : -1) - L.cum;
+  } else {
+    reward = over ? (v2 == 0 ? 1.0 : -1.0) : 0.0;
   }
   if (over) {
-    ko_clear_input(A);
+    L.f.hist = 0;  // ChangeRoundState(KO): ClearInput (BC:296-299)
+    L.f.hold = 0;
     if (p.autoreset_mode == FS_AUTORESET_SAME_STEP) {
-      write_final(A, o, r);
-      ko_and_end_ticks(A);
-      stop_intro_fight<FM, BOT>(A);
-      A.cum = 0.0;
-      A.has_term = false;
+      write_final(L, o, r);
+      reset_burst<FM, BOT>(L, true);
+      L.cum = 0.0;
+      L.has_term = false;
     } else {
-      A.pending = true;
-      A.has_term = true;
+      L.pending = true;
+      L.has_term = true;
     }
   } else {
-    if constexpr (BOT) A.act2 = bot_next_input<FM>(A);  // TrainingManager.Step -> RequestNextInput
-    A.has_term = false;
+    if constexpr (BOT) {  // TrainingManager.Step -> RequestNextInput -> getNextAIInput
+      const float o_x = xpair(L.f.x);
+      const uint32_t o_act = xpair((uint32_t)L.f.act);
+      if (k == 1) L.act = bot_next_input(L.bot, bot_distance<FM>(o_x, L.f.x), o_act);
+    }
+    L.has_term = false;
   }
-  write_main(A, o, r);
-  o.reward[r] = reward;
-  o.terminated[r] = over ? 1 : 0;
-  o.truncated[r] = 0;
+  write_main(L, o, r);
+  if (k == 0) {
+    o.reward[r] = reward;
+    o.terminated[r] = over ? 1 : 0;
+    o.truncated[r] = 0;
+  }
 }
 
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step(StepParams p) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
   stage_tables();
-  if (i >= p.n_envs) return;
+  if (l >= 2 * p.n_envs) return;
   constexpr bool BOT = P2 == FS_P2_BOT;
-  Arena A;
-  load_arena<BOT>(A, p.st, i);
-  for (int k = 0; k < p.n_steps; k++) {
-    const size_t arow = (size_t)k * p.n_envs + i;
-    const size_t orow = (size_t)k * p.out_stride_steps * p.n_envs + i;
-    const uint64_t t = p.t0 + (uint64_t)k;
-    const uint32_t a1 = p.p1 ? p.p1[arow] : hash_action(p.action_seed, i, t, 0);
-    uint32_t a2 = 0;
-    if constexpr (P2 == FS_P2_EXTERNAL) a2 = p.p2 ? p.p2[arow] : hash_action(p.action_seed, i, t, 1);
-    env_step<FM, P2>(A, a1 & 7u, a2 & 7u, p, orow);
+  const int a = l >> 1;
+  const uint32_t k = l & 1;
+  Lane L;
+  load_lane<BOT>(L, p.st, a, k);
+  // This lane's action, software-pipelined one tick ahead: the load for tick t+1
+  // is issued before tick t's output stores, so its wait does not drain them
+  // (loads and stores retire in order on one vmcnt counter).
+  const uint8_t* src = k == 0 ? p.p1 : p.p2;
+  const bool reads = k == 0 || P2 == FS_P2_EXTERNAL;
+  auto fetch = [&](int t) -> uint32_t {
+    if (!reads) return 0u;
+    return src ? src[(size_t)t * p.n_envs + a] : hash_action(p.action_seed, a, p.t0 + (uint64_t)t, k);
+  };
+  uint32_t next = fetch(0);
+  for (int t = 0; t < p.n_steps; t++) {
+    const uint32_t act = next;
+    if (t + 1 < p.n_steps) next = fetch(t + 1);
+    env_step<FM, P2>(L, act & 7u, p, (size_t)t * p.out_stride_steps * p.n_envs + a);
   }
-  store_arena<BOT>(A, p.st, i);
+  store_lane<BOT>(L, p.st, a);
 }
 
 // FootsiesEnv.reset (FE:482-515) / RESET (BC:143-146) / game start (BC:105-128)
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
   stage_tables();
-  if (i >= p.n_envs) return;
-  if (!p.init && p.mask && !p.mask[i]) return;
+  if (l >= 2 * p.n_envs) return;
+  const int a = l >> 1;
+  const uint32_t k = l & 1;
+  if (!p.init && p.mask && !p.mask[a]) return;
   constexpr bool BOT = P2 == FS_P2_BOT;
-  Arena A;
+  Lane L;
   if (p.init) {  // `new Fighter()` defaults (F:73-112), round state Stop
-    for (int k = 0; k < 2; k++) {
-      Fighter& f = k == 0 ? A.f0 : A.f1;
-      f.x = 0.0f;
-      f.hist = 0;
-      f.act = A_STAND;
-      f.frame = f.stun = f.vital = f.guard = f.hits = f.hold = 0;
-      f.buf = f.rsv = NONE;
-      f.in_back = f.prox = f.won = false;
-    }
-    A.frame_count = 0;
-    A.rec_count = A.rec1 = A.rec2 = A.act1 = A.act2 = 0;
-    A.pending = false;
-    A.has_term = true;
-    A.cum = 0.0;
-    A.rng = rng_init((int32_t)(uint32_t)(p.base_seed + (uint64_t)i));
-    A.mplan = A.midx = A.aplan = A.aidx = A.prev_opp = 0;
-    A.prev_dist = 0.0f;
+    L.k = k;
+    L.f.x = 0.0f;
+    L.f.hist = 0;
+    L.f.act = A_STAND;
+    L.f.frame = L.f.stun = L.f.vital = L.f.guard = L.f.hits = L.f.hold = 0;
+    L.f.buf = L.f.rsv = NONE;
+    L.f.in_back = L.f.prox = L.f.won = false;
+    L.frame_count = 0;
+    L.rec_count = L.rec = L.act = 0;
+    L.pending = false;
+    L.has_term = true;
+    L.cum = 0.0;
+    L.bot.rng = rng_init((int32_t)(uint32_t)(p.base_seed + (uint64_t)a));
+    L.bot.mplan = L.bot.midx = L.bot.aplan = L.bot.aidx = L.bot.prev_opp = 0;
+    L.bot.prev_dist = 0.0f;
   } else {
-    load_arena<BOT>(A, p.st, i);
+    load_lane<BOT>(L, p.st, a, k);
   }
-  if (p.seeds) A.rng = rng_init((int32_t)(uint32_t)p.seeds[i]);  // SEED (BC:170-173)
-  const bool hard = p.init || p.flags == FS_RESET_HARD || !A.has_term;
-  if (A.pending) {  // finish the burst Unity ran after the terminal frame
-    ko_and_end_ticks(A);
-    stop_intro_fight<FM, BOT>(A);
-    A.pending = false;
+  if (p.seeds) L.bot.rng = rng_init((int32_t)(uint32_t)p.seeds[a]);  // SEED (BC:170-173)
+  const bool hard = p.init || p.flags == FS_RESET_HARD || !L.has_term;
+  if (L.pending) {  // finish the burst Unity ran after the terminal frame
+    reset_burst<FM, BOT>(L, true);
+    L.pending = false;
   }
-  if (hard) stop_intro_fight<FM, BOT>(A);
-  A.cum = 0.0;
-  A.has_term = p.init ? true : false;
-  write_main(A, p.out, i);
-  p.out.reward[i] = 0.0;
-  p.out.terminated[i] = 0;
-  p.out.truncated[i] = 0;
-  store_arena<BOT>(A, p.st, i);
+  if (hard) reset_burst<FM, BOT>(L, false);
+  L.cum = 0.0;
+  L.has_term = p.init ? true : false;
+  write_main(L, p.out, a);
+  if (k == 0) {
+    p.out.reward[a] = 0.0;
+    p.out.terminated[a] = 0;
+    p.out.truncated[a] = 0;
+  }
+  store_lane<BOT>(L, p.st, a);
 }
 
 // synthetic action stream (fs_hash_actions), one thread per (step, arena)
@@ -1059,15 +1192,14 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-constexpr int kBlock = 256;
 static inline dim3 grid_for(int n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
 
 template <int FM>
 static hipError_t launch_step_fm(const StepParams& p, int p2_mode, hipStream_t s) {
   switch (p2_mode) {
-    case FS_P2_EXTERNAL: hipLaunchKernelGGL((k_step<FM, FS_P2_EXTERNAL>), grid_for(p.n_envs), dim3(kBlock), 0, s, p); break;
-    case FS_P2_BOT: hipLaunchKernelGGL((k_step<FM, FS_P2_BOT>), grid_for(p.n_envs), dim3(kBlock), 0, s, p); break;
-    default: hipLaunchKernelGGL((k_step<FM, FS_P2_NOOP>), grid_for(p.n_envs), dim3(kBlock), 0, s, p); break;
+    case FS_P2_EXTERNAL: hipLaunchKernelGGL((k_step<FM, FS_P2_EXTERNAL>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
+    case FS_P2_BOT: hipLaunchKernelGGL((k_step<FM, FS_P2_BOT>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
+    default: hipLaunchKernelGGL((k_step<FM, FS_P2_NOOP>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
   }
   return hipGetLastError();
 }
@@ -1080,9 +1212,9 @@ hipError_t launch_step(const StepParams& p, int float_mode, int p2_mode, hipStre
 template <int FM>
 static hipError_t launch_reset_fm(const ResetParams& p, int p2_mode, hipStream_t s) {
   switch (p2_mode) {
-    case FS_P2_EXTERNAL: hipLaunchKernelGGL((k_reset<FM, FS_P2_EXTERNAL>), grid_for(p.n_envs), dim3(kBlock), 0, s, p); break;
-    case FS_P2_BOT: hipLaunchKernelGGL((k_reset<FM, FS_P2_BOT>), grid_for(p.n_envs), dim3(kBlock), 0, s, p); break;
-    default: hipLaunchKernelGGL((k_reset<FM, FS_P2_NOOP>), grid_for(p.n_envs), dim3(kBlock), 0, s, p); break;
+    case FS_P2_EXTERNAL: hipLaunchKernelGGL((k_reset<FM, FS_P2_EXTERNAL>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
+    case FS_P2_BOT: hipLaunchKernelGGL((k_reset<FM, FS_P2_BOT>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
+    default: hipLaunchKernelGGL((k_reset<FM, FS_P2_NOOP>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
   }
   return hipGetLastError();
 }

@@ -1,0 +1,17 @@
+#!/bin/bash
+# PMC passes for the step kernel (one counter group per rocprofv3 run; no trace domains
+# combined with --pmc).  Usage (on the GPU box, from the repo root): tools/prof_pmc.sh OUTDIR MODE
+set -e
+OUT=${1:-gpurun_out/pmc}; MODE=${2:-fused}
+ROOT=$(pwd)
+mkdir -p "$OUT"
+cd /tmp; export TMPDIR=/tmp
+run() { name=$1; shift
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/$name" -o run "$@" -- python3 "$ROOT/tools/profile_driver.py" --mode $MODE > "$ROOT/$OUT/$name.log" 2>&1
+}
+run trace
+run fetch --pmc FETCH_SIZE
+run write --pmc WRITE_SIZE
+run sq1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU
+run sq2 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE
+echo done
