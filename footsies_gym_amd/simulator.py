@@ -122,9 +122,10 @@ class FootsiesSim:
         ext = self.p2_mode == "external"
         if ext and p2 is None:
             raise ValueError("p2 actions are required when p2_mode='external'")
-        if isinstance(p1, torch.Tensor) and p1.is_cuda:
-            p1 = _as_u8_device(p1, self.num_envs)
-            p2t = _as_u8_device(p2, self.num_envs) if ext else None
+        on_device = any(isinstance(x, torch.Tensor) and x.is_cuda for x in (p1, p2))
+        if on_device:  # device path: anything on the host is moved over first
+            p1 = _as_u8_device(_to_device(p1, self.device), self.num_envs)
+            p2t = _as_u8_device(_to_device(p2, self.device), self.num_envs) if ext else None
             check(lib().fs_step(self._h, C.c_void_p(p1.data_ptr()),
                                 C.c_void_p(p2t.data_ptr()) if ext else None, _abi.FS_ACT_DEVICE), self._h)
         else:
@@ -217,6 +218,13 @@ def _host(a):
     if isinstance(a, torch.Tensor):
         return a.detach().cpu().numpy()
     return a
+
+
+def _to_device(a, device):
+    torch = _torch()
+    if isinstance(a, torch.Tensor):
+        return a.to(device)
+    return torch.as_tensor(encode_actions(np.asarray(a)), device=device)
 
 
 def _as_u8_device(t, n):

@@ -1,0 +1,221 @@
+"""FootsiesVectorEnv: the reference FootsiesEnv surface, vectorized over N arenas on one GPU.
+
+Reference: footsies-gym/footsies_gym/envs/footsies.py (FE).  Per arena, the
+observation, info, reward, termination and reset handshake are those of
+``FootsiesEnv.reset`` / ``FootsiesEnv.step`` (FE:482-570); they are computed on
+the GPU by libfootsies.so and only converted to the gymnasium dtypes here.
+
+Differences from the reference, by design:
+  * one object steps N arenas; actions are (N,3) booleans or (N,) ints 0..7;
+  * no game process, sockets, fast-forward or sync modes -- the simulation is
+    in-process and always "synced" (FE:44, 225-228);
+  * auto-reset: ``autoreset_mode="same_step"`` follows gymnasium 0.29's
+    SyncVectorEnv (returned obs is the new episode's first obs, the terminal one
+    is in ``infos["final_observation"]``); ``"next_step"`` follows gymnasium 1.x.
+"""
+import numpy as np
+
+from . import spaces as sp
+from .simulator import FootsiesSim, decode_actions, encode_actions
+
+
+def obs_info_from_outputs(out, prefix=""):
+    """Host-side view of one set of kernel outputs -> (obs, info) batches with the
+    reference dtypes: MultiDiscrete -> int64, Box -> float32 (FE:157-168, 336-380)."""
+    g = out[prefix + "guard"]
+    obs = {
+        "guard": np.asarray(g, dtype=np.int64),
+        "move": np.asarray(out[prefix + "move"], dtype=np.int64),
+        "move_frame": np.asarray(out[prefix + "move_frame"], dtype=np.float32),
+        "position": np.asarray(out[prefix + "position"], dtype=np.float32),
+    }
+    act = np.asarray(out[prefix + "action"])
+    hs = np.asarray(out[prefix + "hitstun"], dtype=np.int64)
+    info = {
+        "frame": np.asarray(out[prefix + "frame"], dtype=np.int64),
+        "p1_action": decode_actions(act[:, 0]),
+        "p2_action": decode_actions(act[:, 1]),
+        "p1_hitstun": hs[:, 0],
+        "p2_hitstun": hs[:, 1],
+    }
+    info.update({k: v.copy() for k, v in obs.items()})  # FE:379 puts a copy of the obs in the info
+    return obs, info
+
+
+def step_result_from_outputs(out, autoreset_mode="same_step"):
+    """(obs, rewards, terminations, truncations, infos) from host copies of the outputs."""
+    obs, info = obs_info_from_outputs(out)
+    rewards = np.asarray(out["reward"], dtype=np.float64)
+    term = np.asarray(out["terminated"]).astype(bool)
+    trunc = np.asarray(out["truncated"]).astype(bool)
+    if autoreset_mode == "same_step" and term.any():
+        fobs, finfo = obs_info_from_outputs(out, prefix="final_")
+        idx = np.nonzero(term)[0]
+        final_obs = np.empty(len(term), dtype=object)
+        final_info = np.empty(len(term), dtype=object)
+        for i in idx:
+            final_obs[i] = {k: v[i] for k, v in fobs.items()}
+            final_info[i] = {k: v[i] for k, v in finfo.items()}
+        info["final_observation"] = final_obs
+        info["_final_observation"] = term.copy()
+        info["final_info"] = final_info
+        info["_final_info"] = term.copy()
+    return obs, rewards, term, trunc, info
+
+
+class FootsiesVectorEnv:
+    """N FOOTSIES arenas as one vector environment.
+
+    Parameters follow FootsiesEnv.__init__ (FE:34-53) where they still have a
+    meaning: ``frame_delay`` (only 0), ``dense_reward``, ``opponent``:
+      * ``None`` -> the in-game scripted bot as P2 (FE:236-237, ``--p2-bot``);
+      * a callable ``opponent(obs, info) -> actions`` -> P2 driven by that policy,
+        called every step with the most recent batched obs/info (FE:525-527);
+      * ``"noop"`` -> P2 never presses anything.
+    ``output="torch"`` returns device tensors (zero-copy) instead of numpy.
+    """
+
+    metadata = {"render_modes": [], "render_fps": 60}
+
+    def __init__(self, num_envs, device=0, opponent=None, dense_reward=True, frame_delay=0,
+                 autoreset_mode="same_step", float_mode="strict", seed=0, vs_player=False, by_example=False,
+                 output="numpy"):
+        if vs_player:
+            raise ValueError("vs_player needs a human at the game window; not available in the simulator")
+        if by_example:
+            raise ValueError("by_example (the bot playing P1) is not supported")
+        if frame_delay != 0:
+            raise ValueError("frame_delay > 0 is not supported yet (FE:126-131)")
+        if output not in ("numpy", "torch"):
+            raise ValueError("output must be 'numpy' or 'torch'")
+        self.num_envs = int(num_envs)
+        self.output = output
+        self.autoreset_mode = autoreset_mode
+        self.dense_reward = dense_reward
+        self._opponent = opponent
+        p2 = "bot" if opponent is None else ("noop" if isinstance(opponent, str) and opponent == "noop" else "external")
+        if p2 == "external" and not callable(opponent):
+            raise ValueError("opponent must be None, 'noop' or a callable(obs, info) -> actions")
+        self.sim = FootsiesSim(self.num_envs, device=device, p2_mode=p2, dense_reward=dense_reward,
+                               float_mode=float_mode, autoreset_mode=autoreset_mode, seed=seed,
+                               frame_delay=frame_delay)
+        self.single_observation_space = sp.single_observation_space()
+        self.single_action_space = sp.single_action_space()
+        self.observation_space = sp.batch_observation_space(self.num_envs)
+        self.action_space = sp.batch_action_space(self.num_envs)
+        self.reward_range = (-1, 1)
+        self._last = None  # most recent (obs, info) for the opponent callable
+
+    # -- gymnasium.vector.VectorEnv API ---------------------------------------------------
+    def reset(self, *, seed=None, options=None):
+        """FootsiesEnv.reset on every arena (or ``options["mask"]``).  ``seed``: int (arena i
+        gets seed + i) or a sequence of N seeds -> Random.InitState of each arena's bot.
+        ``options["hard"]=True`` forces the RESET command even after a terminated step."""
+        options = options or {}
+        seeds = None
+        if seed is not None:
+            seeds = (np.asarray(seed, dtype=np.uint64) if np.ndim(seed) else
+                     np.uint64(seed) + np.arange(self.num_envs, dtype=np.uint64))
+        out = self.sim.reset(seeds=seeds, mask=options.get("mask"), hard=bool(options.get("hard", False)))
+        if self.output == "torch":
+            self._last = (out, None)
+            return {k: out[k] for k in ("guard", "move", "move_frame", "position")}, out
+        obs, info = obs_info_from_outputs(self.sim.outputs_numpy())
+        self._last = (obs, info)
+        return obs, info
+
+    def step(self, actions):
+        p2 = None
+        if self.sim.p2_mode == "external":
+            p2 = self._opponent(*self._last) if self._last is not None else np.zeros(self.num_envs, np.uint8)
+        out = self.sim.step(actions, p2)
+        if self.output == "torch":
+            obs = {k: out[k] for k in ("guard", "move", "move_frame", "position")}
+            self._last = (obs, out)
+            return obs, out["reward"], out["terminated"], out["truncated"], out
+        obs, rew, term, trunc, info = step_result_from_outputs(self.sim.outputs_numpy(), self.autoreset_mode)
+        self._last = (obs, info)
+        return obs, rew, term, trunc, info
+
+    def close(self):
+        self.sim.close()
+
+    # -- FootsiesEnv extras (FE:432-480) ------------------------------------------------
+    def save_battle_state(self):
+        """STATE_SAVE (BC:148-151): canonical per-arena state, see fs_arena_state."""
+        return self.sim.get_state()
+
+    def load_battle_state(self, state):
+        """STATE_LOAD (BC:153-156)."""
+        self.sim.set_state(state)
+
+    @property
+    def most_recent_observation(self):
+        return None if self._last is None else self._last[0]
+
+    @property
+    def most_recent_info(self):
+        return None if self._last is None else self._last[1]
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class FootsiesEnv:
+    """Single-environment adapter with the reference FootsiesEnv API (FE:20-578) over
+    one arena: tuples of Python ints/floats in, reference-shaped dicts out."""
+
+    metadata = {"render_modes": "human", "render_fps": 60}
+
+    def __init__(self, frame_delay=0, dense_reward=True, opponent=None, device=0, seed=0, **_unused):
+        self._opp = opponent
+        opp = None
+        if opponent is not None:
+            opp = (lambda obs, info: np.array([encode_actions([self._opp(obs, info)])[0]], np.uint8))
+        # next_step auto-reset keeps FE's handshake: a terminal step() returns the terminal
+        # obs and the agent's reset() then finds the game already at state(-1) (no RESET)
+        self.venv = FootsiesVectorEnv(1, device=device, opponent=opp, dense_reward=dense_reward,
+                                      frame_delay=frame_delay, seed=seed, autoreset_mode="next_step")
+        self.observation_space = self.venv.single_observation_space
+        self.action_space = self.venv.single_action_space
+        self.reward_range = (-1, 1)
+        self._most_recent_observation = None
+        self._most_recent_info = None
+
+    @staticmethod
+    def _py(obs, info):
+        def pos(x):  # EnvironmentState floats travel as shortest round-trip JSON text (FE:319)
+            return float(str(np.float32(x)))
+        o = {"guard": tuple(int(v) for v in obs["guard"][0]), "move": tuple(int(v) for v in obs["move"][0]),
+             "move_frame": tuple(int(v) for v in obs["move_frame"][0]),
+             "position": tuple(pos(v) for v in obs["position"][0])}
+        i = {"frame": int(info["frame"][0]), "p1_action": tuple(bool(v) for v in info["p1_action"][0]),
+             "p2_action": tuple(bool(v) for v in info["p2_action"][0]), "p1_hitstun": int(info["p1_hitstun"][0]),
+             "p2_hitstun": int(info["p2_hitstun"][0]), **o}
+        return o, i
+
+    def reset(self, *, seed=None, options=None):
+        obs, info = self.venv.reset(seed=seed, options=options)
+        o, i = self._py(obs, info)
+        self._most_recent_observation, self._most_recent_info = dict(o), dict(i)
+        return o, i
+
+    def step(self, action):
+        obs, rew, term, trunc, info = self.venv.step(np.asarray([action]).reshape(1, 3))
+        o, i = self._py(obs, info)
+        self._most_recent_observation, self._most_recent_info = dict(o), dict(i)
+        return o, float(rew[0]), bool(term[0]), False, i
+
+    def close(self):
+        self.venv.close()
+
+    @property
+    def most_recent_observation(self):
+        return self._most_recent_observation
+
+    @property
+    def most_recent_info(self):
+        return self._most_recent_info

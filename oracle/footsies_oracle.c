@@ -1129,7 +1129,7 @@ OR_EXPORT int or_create(const fs_config* cfg, or_handle* out) {
   C->f_move_frame = xcalloc(2 * n, sizeof(float));
   C->f_position = xcalloc(2 * n, sizeof(float));
   C->f_frame = xcalloc(n, sizeof(int32_t));
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (C->n >= 1024)
   for (int i = 0; i < n; i++) {
     arena_t* A = &C->a[i];
     new_fighter(&A->f[0]);
@@ -1149,7 +1149,7 @@ OR_EXPORT int or_create(const fs_config* cfg, or_handle* out) {
 
 OR_EXPORT int or_reset(or_handle C, const uint64_t* seeds, const uint8_t* mask, int flags) {
   if (!C) return FS_E_INVALID;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (C->n >= 1024)
   for (int i = 0; i < C->n; i++) {
     if (mask && !mask[i]) continue;
     int hard = (flags == FS_RESET_HARD) || !C->a[i].has_terminated;
@@ -1161,7 +1161,7 @@ OR_EXPORT int or_reset(or_handle C, const uint64_t* seeds, const uint8_t* mask, 
 OR_EXPORT int or_step(or_handle C, const uint8_t* p1, const uint8_t* p2) {
   if (!C || !p1) return FS_E_INVALID;
   if (C->cfg.p2_mode == FS_P2_EXTERNAL && !p2) return FS_E_INVALID;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (C->n >= 1024)
   for (int i = 0; i < C->n; i++) fe_step_arena(C, i, p1[i], p2 ? p2[i] : 0);
   C->steps++;
   return FS_OK;
@@ -1182,7 +1182,7 @@ OR_EXPORT uint8_t or_hash_action(uint64_t seed, uint64_t env, uint64_t t, int pl
 OR_EXPORT int or_step_n_hashed(or_handle C, int n, uint64_t action_seed) {
   if (!C || n < 0) return FS_E_INVALID;
   uint64_t t0 = C->steps;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (C->n >= 1024)
   for (int i = 0; i < C->n; i++)
     for (int k = 0; k < n; k++)
       fe_step_arena(C, i, or_hash_action(action_seed, (uint64_t)i, t0 + (uint64_t)k, 0),

@@ -1,0 +1,98 @@
+"""The C-ABI library: loads, exports every symbol include/footsies.h declares, struct layouts
+agree between C (gcc on the header) and the ctypes mirror, and creation without a GPU fails
+loudly with a message instead of falling back to anything."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from footsies_gym_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "footsies.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fs_[a-z_]+)\(", text, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from footsies_gym_amd import build
+    build.build()
+    return C.CDLL(build.LIB)
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _abi.LIB_FUNCTIONS, "ctypes binding misses %s" % n
+    assert set(_abi.LIB_FUNCTIONS) == set(names)
+
+
+def test_abi_version(lib):
+    lib.fs_abi_version.restype = C.c_int
+    assert lib.fs_abi_version() == _abi.FS_ABI_VERSION
+
+
+def _c_layout(tmp_path):
+    structs = {"fs_config": _abi.fs_config, "fs_outputs": _abi.fs_outputs, "fs_env_state": _abi.fs_env_state,
+               "fs_fighter_state": _abi.fs_fighter_state, "fs_arena_state": _abi.fs_arena_state}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "footsies.h"', "int main(void){"]
+    for s, cls in structs.items():
+        lines.append('printf("%s size %%zu\\n", sizeof(%s));' % (s, s))
+        for f, _ in cls._fields_:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (s, f, s, f))
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    return structs, dict(line.rsplit(" ", 1) for line in out.strip().splitlines())
+
+
+def test_struct_layouts_match_ctypes(tmp_path):
+    structs, c = _c_layout(tmp_path)
+    for s, cls in structs.items():
+        assert int(c["%s size" % s]) == C.sizeof(cls), s
+        for f, _ in cls._fields_:
+            assert int(c["%s.%s" % (s, f)]) == getattr(cls, f).offset, (s, f)
+
+
+def test_create_without_gpu_fails_loudly(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    lib.fs_create.argtypes = [C.POINTER(_abi.fs_config), C.POINTER(C.c_void_p)]
+    lib.fs_last_error.restype = C.c_char_p
+    lib.fs_last_error.argtypes = [C.c_void_p]
+    h = C.c_void_p()
+    cfg = _abi.fs_config(num_envs=4)
+    rc = lib.fs_create(C.byref(cfg), C.byref(h))
+    assert rc == _abi.FS_E_DEVICE
+    assert not h.value
+    assert lib.fs_last_error(None)
+
+
+def test_invalid_configs_rejected(lib):
+    lib.fs_create.argtypes = [C.POINTER(_abi.fs_config), C.POINTER(C.c_void_p)]
+    h = C.c_void_p()
+    for kw, code in [({"num_envs": 0}, _abi.FS_E_INVALID), ({"num_envs": 4, "p2_mode": 9}, _abi.FS_E_INVALID),
+                     ({"num_envs": 4, "frame_delay": 2}, _abi.FS_E_UNSUPPORTED),
+                     ({"num_envs": 4, "float_mode": 7}, _abi.FS_E_INVALID)]:
+        assert lib.fs_create(C.byref(_abi.fs_config(**kw)), C.byref(h)) == code, kw
+
+
+def test_simulator_requires_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from footsies_gym_amd.simulator import FootsiesSim
+    with pytest.raises(RuntimeError):
+        FootsiesSim(8)

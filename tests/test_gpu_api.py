@@ -1,0 +1,160 @@
+"""The HIP product path through its public surfaces: KATs, the reference-FE golden vectors,
+fused multi-tick launches, state save/load, hashed actions, VectorEnv / FootsiesEnv."""
+import numpy as np
+import pytest
+
+from footsies_gym_amd import _abi
+from tests import golden_utils as gu
+from tests import kat_scenarios as kat
+from tests.gpu_backend import SimBackend, make
+from tests.parity_utils import compare_outputs, compare_states
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", sorted(kat.ALL))
+def test_kat_gpu(name):
+    kat.ALL[name](SimBackend(1))
+
+
+@pytest.mark.parametrize("name", gu.CASES)
+def test_golden_reference_fe_gpu(name):
+    c = gu.case(gu.load(), name)
+    gu.replay_next_step(c, make)
+    gu.replay_same_step(c, make)
+
+
+def test_step_n_trajectory_matches_single_steps(oracle_lib):
+    """fs_step_n with a [n][N] trajectory == n fs_step calls == the oracle."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    N, T = 1000, 150
+    a = FootsiesSim(N, p2_mode="external", seed=3)
+    b = FootsiesSim(N, p2_mode="external", seed=3)
+    p1, p2 = a.hash_actions(T, seed=77)
+    traj = a.alloc_trajectory(T)
+    a.step_n(T, p1, p2, trajectory=traj)
+    torch.cuda.synchronize()
+    tr = {k: v.cpu().numpy() for k, v in traj.items()}
+    ora = oracle_lib.Oracle(N, p2_mode=_abi.FS_P2_EXTERNAL, base_seed=3)
+    h1, h2 = p1.cpu().numpy(), p2.cpu().numpy()
+    for t in range(T):
+        b.step(p1[t], p2[t])
+        got = b.outputs_numpy()
+        exp = ora.step(h1[t], h2[t])
+        compare_outputs(exp, got, step=t)
+        compare_outputs(exp, {k: v[t] for k, v in tr.items()}, step=t)
+    compare_states(ora.state(), a.get_state())
+    compare_states(ora.state(), b.get_state())
+
+
+def test_hashed_actions_match_host_stream(oracle_lib):
+    """fs_hash_actions / in-kernel hashing == the splitmix64 stream of SURVEY.md §8(d)."""
+    from footsies_gym_amd.simulator import FootsiesSim
+    N = 3000
+    s = FootsiesSim(N, p2_mode="external")
+    p1, p2 = s.hash_actions(4, seed=0x5EED, t0=10)
+    for t in range(4):
+        assert np.array_equal(p1[t].cpu().numpy(), oracle_lib.hash_actions(0x5EED, N, 10 + t, 0))
+        assert np.array_equal(p2[t].cpu().numpy(), oracle_lib.hash_actions(0x5EED, N, 10 + t, 1))
+    # in-kernel hashed actions (no action arrays) follow the same stream
+    ora = oracle_lib.Oracle(N, p2_mode=_abi.FS_P2_EXTERNAL)
+    s2 = FootsiesSim(N, p2_mode="external")
+    s2.step_n(25, None, None, action_seed=0x5EED)
+    ora.step_n_hashed(25, 0x5EED)
+    compare_states(ora.state(), s2.get_state())
+
+
+@pytest.mark.parametrize("p2", ["bot", "external"])
+def test_state_save_load_roundtrip(oracle_lib, p2):
+    """fs_get_state -> fs_set_state into a fresh handle continues bit-identically."""
+    from footsies_gym_amd.simulator import FootsiesSim
+    N = 700
+    a = FootsiesSim(N, p2_mode=p2, seed=1)
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        a.step(rng.integers(0, 8, N), rng.integers(0, 8, N) if p2 == "external" else None)
+    st = a.get_state()
+    b = FootsiesSim(N, p2_mode=p2, seed=999)
+    b.set_state(st)
+    compare_states(st, b.get_state())
+    for t in range(200):
+        x1, x2 = rng.integers(0, 8, N), rng.integers(0, 8, N)
+        a.step(x1, x2 if p2 == "external" else None)
+        b.step(x1, x2 if p2 == "external" else None)
+        oa, ob = a.outputs_numpy(), b.outputs_numpy()
+        compare_outputs(oa, ob, step=t)
+
+
+def test_device_actions_and_stream_interop():
+    """Device-tensor actions produced by torch kernels on torch's stream need no sync."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    N = 4096
+    a = FootsiesSim(N, p2_mode="external", seed=5)
+    b = FootsiesSim(N, p2_mode="external", seed=5)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(50):
+        x1 = torch.randint(0, 8, (N,), device="cuda", dtype=torch.uint8, generator=g)
+        x2 = torch.randint(0, 8, (N,), device="cuda", dtype=torch.uint8, generator=g)
+        a.step(x1, x2)  # device path
+        b.step(x1.cpu().numpy(), x2.cpu().numpy())  # host path
+        oa = {k: v.clone() for k, v in a.outputs().items()}
+        ob = b.outputs_numpy()
+        compare_outputs(ob, {k: v.cpu().numpy() for k, v in oa.items()})
+
+
+def test_vector_env_surface():
+    from footsies_gym_amd.vector_env import FootsiesVectorEnv
+    env = FootsiesVectorEnv(64, seed=0)
+    obs, info = env.reset(seed=42)
+    assert obs["guard"].shape == (64, 2) and obs["guard"].dtype == np.int64
+    assert (obs["position"][:, 0] == -2).all() and (info["frame"] == -1).all()
+    assert env.observation_space.contains(obs)
+    total_eps = 0
+    rng = np.random.default_rng(0)
+    for _ in range(400):
+        obs, rew, term, trunc, info = env.step(rng.integers(0, 2, (64, 3)).astype(bool))
+        assert rew.dtype == np.float64 and term.dtype == bool and not trunc.any()
+        if term.any():
+            total_eps += int(term.sum())
+            i = int(np.nonzero(term)[0][0])
+            assert info["final_observation"][i] is not None
+            assert info["frame"][i] == -1  # same-step auto-reset: obs is the new episode's state(-1)
+            assert obs["move"][i].tolist() == [0, 0]
+        assert env.observation_space.contains(obs)
+    assert total_eps > 0
+    env.close()
+
+
+def test_vector_env_custom_opponent_and_torch_output():
+    import torch
+    from footsies_gym_amd.vector_env import FootsiesVectorEnv
+    calls = []
+
+    def opponent(obs, info):
+        calls.append(1)
+        return np.full(16, 4, np.uint8)  # always attack
+    env = FootsiesVectorEnv(16, opponent=opponent, output="torch")
+    obs, _ = env.reset()
+    o, r, te, tr, info = env.step(torch.zeros(16, dtype=torch.uint8, device="cuda"))
+    assert calls and o["guard"].is_cuda and r.dtype == torch.float64
+    env.close()
+
+
+def test_single_env_adapter_matches_reference_api():
+    from footsies_gym_amd.vector_env import FootsiesEnv
+    env = FootsiesEnv(dense_reward=True)
+    obs, info = env.reset(seed=0)
+    assert obs == {"guard": (3, 3), "move": (0, 0), "move_frame": (0, 0), "position": (-2.0, 2.0)}
+    assert info["frame"] == -1 and info["p1_action"] == (False, False, False)
+    done = False
+    n = 0
+    while not done and n < 5000:
+        obs, reward, done, trunc, info = env.step((False, False, True) if n % 2 else (False, True, False))
+        assert isinstance(reward, float) and trunc is False
+        n += 1
+    assert done
+    obs, info = env.reset()
+    assert info["frame"] == -1
+    env.close()

@@ -1,0 +1,78 @@
+"""Host-side logic of the Python layer (no GPU): action encoding (TrainingRemoteActor.cs:112-116),
+info decoding (state.py:26-36), spaces (footsies.py:157-171), and the output -> (obs, info,
+reward, ...) conversion including gymnasium 0.29 same-step final_observation."""
+import numpy as np
+
+from footsies_gym_amd import spaces
+from footsies_gym_amd.simulator import decode_actions, encode_actions
+from footsies_gym_amd.vector_env import obs_info_from_outputs, step_result_from_outputs
+
+
+def test_encode_decode_roundtrip():
+    bools = np.array([[b & 1, b & 2, b & 4] for b in range(8)]) != 0
+    bits = encode_actions(bools)
+    assert bits.tolist() == list(range(8))
+    assert encode_actions(np.arange(8)).tolist() == list(range(8))
+    assert np.array_equal(decode_actions(bits), bools)
+    # non-zero bytes count as pressed, like the game's 3-byte action message
+    assert encode_actions(np.array([[5, 0, 255]])).tolist() == [5]
+
+
+def test_encode_rejects_bad_shapes():
+    import pytest
+    with pytest.raises(ValueError):
+        encode_actions(np.zeros((4, 2)))
+    with pytest.raises(ValueError):
+        encode_actions(np.array([8]))
+
+
+def test_spaces():
+    obs = spaces.single_observation_space()
+    assert obs["guard"].contains(np.array([3, 0]))
+    assert not obs["guard"].contains(np.array([4, 0]))
+    assert obs["move"].contains(np.array([14, 0])) and not obs["move"].contains(np.array([15, 0]))
+    assert float(obs["move_frame"].high[0]) == 55.0  # max duration without DEAD/WIN (B_SPECIAL)
+    assert obs["position"].contains(np.array([-4.6, 4.6], np.float32))
+    assert spaces.single_action_space().shape == (3,)
+    b = spaces.batch_observation_space(5)
+    assert b["guard"].shape == (5, 2)
+
+
+def fake_outputs(n, term_rows=()):
+    rng = np.random.default_rng(0)
+    out = {
+        "guard": rng.integers(0, 4, (n, 2)).astype(np.uint8), "move": rng.integers(0, 15, (n, 2)).astype(np.uint8),
+        "move_frame": rng.integers(0, 40, (n, 2)).astype(np.float32),
+        "position": rng.uniform(-4, 4, (n, 2)).astype(np.float32), "reward": rng.normal(size=n),
+        "terminated": np.zeros(n, np.uint8), "truncated": np.zeros(n, np.uint8),
+        "frame": rng.integers(-1, 500, n).astype(np.int32), "action": rng.integers(0, 8, (n, 2)).astype(np.uint8),
+        "hitstun": rng.integers(0, 30, (n, 2)).astype(np.uint8)}
+    for k in list(out):
+        if k not in ("reward", "terminated", "truncated"):
+            out["final_" + k] = out[k].copy() + (1 if out[k].dtype != np.float32 else 0.5)
+    for r in term_rows:
+        out["terminated"][r] = 1
+    return out
+
+
+def test_obs_info_conversion():
+    out = fake_outputs(6)
+    obs, info = obs_info_from_outputs(out)
+    assert obs["guard"].dtype == np.int64 and obs["move"].dtype == np.int64
+    assert obs["position"].dtype == np.float32 and obs["move_frame"].dtype == np.float32
+    assert np.array_equal(info["p1_action"], decode_actions(out["action"][:, 0]))
+    assert np.array_equal(info["p2_hitstun"], out["hitstun"][:, 1])
+    for k in ("guard", "move", "move_frame", "position"):  # FE:379 copies the obs into the info
+        assert np.array_equal(info[k], obs[k])
+
+
+def test_same_step_final_observation():
+    out = fake_outputs(5, term_rows=(1, 3))
+    obs, rew, term, trunc, info = step_result_from_outputs(out, "same_step")
+    assert term.tolist() == [False, True, False, True, False]
+    assert info["_final_observation"].tolist() == term.tolist()
+    assert info["final_observation"][0] is None
+    assert np.array_equal(info["final_observation"][3]["guard"], out["final_guard"][3].astype(np.int64))
+    assert info["final_info"][1]["frame"] == out["final_frame"][1]
+    _, _, _, _, info2 = step_result_from_outputs(out, "next_step")
+    assert "final_observation" not in info2

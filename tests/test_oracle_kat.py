@@ -1,0 +1,11 @@
+"""Known-answer scenarios (tests/kat_scenarios.py) on the CPU oracle."""
+import pytest
+
+from footsies_gym_amd import _abi
+from tests import kat_scenarios as kat
+
+
+@pytest.mark.parametrize("name", sorted(kat.ALL))
+def test_kat_oracle(oracle_lib, name):
+    o = oracle_lib.Oracle(1, p2_mode=_abi.FS_P2_EXTERNAL, autoreset_mode=_abi.FS_AUTORESET_SAME_STEP)
+    kat.ALL[name](o)
