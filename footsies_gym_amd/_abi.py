@@ -31,6 +31,7 @@ FS_STREAM_OWN = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)
 
 FS_RESET_HARD = 0
 FS_RESET_IF_NEEDED = 1
+FS_RESET_SEED_ONLY = 2
 
 # InputDefine (Assets/Script/InputData.cs:8-14)
 IN_LEFT, IN_RIGHT, IN_ATTACK = 1, 2, 4

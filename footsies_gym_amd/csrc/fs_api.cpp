@@ -214,7 +214,9 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
 
 FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int flags) {
   if (!h) return FS_E_INVALID;
-  if (flags != FS_RESET_HARD && flags != FS_RESET_IF_NEEDED) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
+  if (flags != FS_RESET_HARD && flags != FS_RESET_IF_NEEDED && flags != FS_RESET_SEED_ONLY)
+    return set_err(h, FS_E_INVALID, "bad flags %d", flags);
+  if (flags == FS_RESET_SEED_ONLY && !seeds) return FS_OK;
   int rc;
   if ((rc = use_device(h))) return rc;
   if ((rc = staging_wait(h))) return rc;

@@ -1,16 +1,21 @@
-// fs_kernels.hip -- HIP kernels for gfx950 (MI355X): one lane = one FOOTSIES arena.
+// fs_kernels.hip -- HIP kernels for gfx950 (MI355X): the FOOTSIES Fight tick for N arenas.
 //
 // A Fight tick of the reference (BattleCore.FixedUpdate Fight branch ->
 // UpdateFightState, Assets/Script/BattleCore.cs:201-220, 347-364) is restated
-// over a bit-packed, struct-of-arrays arena state that lives in HBM:
+// over a bit-packed, struct-of-arrays arena state in HBM, two lanes per arena
+// (one fighter each, partner values exchanged with DPP):
 //
-//   load (5 coalesced 8/16-B vectors per lane) -> tick in registers -> store
+//   load (coalesced 4/8/16-B per lane) -> n ticks in registers -> store
 //
-// Frame data is the dense per-(action, frame) form generated into fs_tables.h
-// (window scans of ActionData.cs:87-168 resolved offline).  The 180-deep input
-// histories (Fighter.cs:98-101) are replaced by a 16-frame Left/Right shift
-// register plus a saturating attack-hold counter: the reference only ever
-// reads input[0..16] for dashes (Fighter.cs:585-635, dashAllowFrame 9) and
+// Frame data is one ~6 KB image staged into LDS per block: per action a 16-B
+// ActionInfo (frame count, loop, cancel window), and per (action, frame) an
+// index into 51 de-duplicated 96-B frame records holding every box's geometry,
+// the velocity and the hitbox attack bits -- the window scans of
+// ActionData.cs:87-168 resolved offline (tools/gen_tables.py).  A tick needs
+// four dependent LDS round trips: action info, requested actions' infos, record
+// index, record.  The 180-deep input histories (Fighter.cs:98-101) are a 16-frame
+// Left/Right shift register plus a saturating attack-hold counter: the reference
+// only reads input[0..16] for dashes (Fighter.cs:585-635, dashAllowFrame 9) and
 // "attack held on input[1..59]" for the charge special (Fighter.cs:569-583).
 //
 // Float arithmetic follows the C# expression order with every binary32
@@ -81,10 +86,11 @@ struct Fighter {
   uint32_t hist;  // raw Left/Right bits of input[0..15]
   int act, frame, stun, vital, guard, hits, buf, rsv, hold;
   bool in_back, prox, won;
-  // boxes of this tick (UpdateBoxes, F:671-697), x only: y == rect.y since position.y == 0
-  uint32_t hitset, hurtset;
-  int push_rect;
-  float hx0, hx1, ux0, ux1, px;
+  // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
+  // the fighter their world x (y == rect.y since position.y is always 0)
+  int rec;        // FrameRec index of (action, frame)
+  uint32_t info;  // FrameRec::info (box counts, hitbox attack bits)
+  float px, ux0, ux1, hx0, hx1;
 };
 
 struct Arena {
@@ -275,7 +281,7 @@ __device__ __forceinline__ InputEval update_input(Fighter& f, uint32_t in, int k
 // ---------------------------------------------------------------------------
 // action state machine (F:140-166, 201-286, 472-510, 546-563)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void set_action(Fighter& f, int a) {
+__device__ __forceinline__ void set_action(Fighter& f, int a) {  // SetCurrentAction (F:546-563)
   f.act = a;
   f.frame = 0;
   f.hits = 0;
@@ -283,91 +289,109 @@ __device__ __forceinline__ void set_action(Fighter& f, int a) {
   f.rsv = NONE;
 }
 
-__device__ __forceinline__ void request_action(Fighter& f, int a) {
-  const ActionInfo ai = sT.action[f.act];
-  if (f.frame >= ai.frame_count) {
-    set_action(f, a);
-    return;
-  }
-  if (f.act == a) return;
-  if (ai.always_cancel) {
-    set_action(f, a);
-    return;
-  }
-  const uint32_t row = sT.rows[ai.row + f.frame];
-  if (sT.cancel[(row >> 21) & 15] & (1u << a)) f.buf = a;  // buffer or execute window lists `a`
+// ActionInfo (fs_tables.h) travels in registers as its raw 16 bytes: selecting
+// between two struct values (HIP's uint4 included) would go through scratch memory.
+typedef uint32_t AInfo __attribute__((ext_vector_type(4)));  // a native vector: selects stay in registers
+__device__ __forceinline__ AInfo action_info(int a) { return reinterpret_cast<const AInfo*>(sT.action)[a]; }
+__device__ __forceinline__ int ai_frame_count(AInfo i) { return (int)(int16_t)(i.x & 0xffffu); }
+__device__ __forceinline__ int ai_loop_from(AInfo i) { return (int)(int16_t)(i.x >> 16); }
+__device__ __forceinline__ bool ai_always_cancel(AInfo i) { return (i.y & 0xffu) != 0; }
+__device__ __forceinline__ int ai_cancel_lo(AInfo i) { return (int)((i.y >> 16) & 0xffu); }
+__device__ __forceinline__ int ai_cancel_hi(AInfo i) { return (int)(i.y >> 24); }
+__device__ __forceinline__ uint32_t ai_cancel_mask(AInfo i) { return i.z; }
+static_assert(sizeof(ActionInfo) == 16, "ActionInfo must be 16 bytes");
+
+// RequestAction (F:472-510), branch-free.  `ai` is the ActionInfo of f.act (kept
+// current across a chain of requests), `an` the one of the requested action `a`,
+// `valid` = false turns the call into a no-op.  The cancel windows of an action
+// are one frame range with one target mask (asserted by tools/gen_tables.py); a
+// buffer or execute window listing `a` leaves bufferActionID = a.
+__device__ __forceinline__ void request_action(Fighter& f, AInfo& ai, int a, AInfo an, bool valid) {
+  const bool ended = f.frame >= ai_frame_count(ai);
+  const bool same = f.act == a;
+  const bool take = valid & (ended | (!same & ai_always_cancel(ai)));
+  const bool buffer = valid & !take & !same & (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai)) &
+                      (((ai_cancel_mask(ai) >> a) & 1u) != 0);
+  f.act = take ? a : f.act;
+  f.frame = take ? 0 : f.frame;
+  f.hits = take ? 0 : f.hits;
+  f.rsv = take ? NONE : f.rsv;
+  f.buf = take ? NONE : (buffer ? a : f.buf);
+  ai = take ? an : ai;
 }
 
-__device__ __forceinline__ void increment_action_frame(Fighter& f) {
-  if (f.stun > 0) {
-    f.stun--;
-    return;
-  }
-  f.frame++;
-  const ActionInfo ai = sT.action[f.act];
-  if (f.frame >= ai.frame_count && ai.loop_from >= 0) f.frame = ai.loop_from;
+// IncrementActionFrame (F:140-166); `ai` = ActionInfo of f.act
+__device__ __forceinline__ void increment_action_frame(Fighter& f, AInfo ai) {
+  const bool stunned = f.stun > 0;
+  f.stun -= stunned ? 1 : 0;
+  const int next = f.frame + 1;
+  const int loop_from = ai_loop_from(ai);
+  const int looped = (next >= ai_frame_count(ai) && loop_from >= 0) ? loop_from : next;
+  f.frame = stunned ? f.frame : looped;
 }
 
-__device__ __forceinline__ void update_action_request(Fighter& f, const InputEval& e) {
-  if (f.won) {
-    request_action(f, A_WIN);
+// UpdateActionRequest (F:201-286).  Every request target is decided from the inputs
+// and the state before the first request, so the four ActionInfo reads are issued
+// together; the request chain itself is branch-free.
+__device__ __forceinline__ void update_action_request(Fighter& f, const InputEval& e, AInfo& ai) {
+  if (f.won) {  // F:204-208 (hasWon is only set between KO and the next SetupBattleStart)
+    request_action(f, ai, A_WIN, action_info(A_WIN), true);
     return;
   }
-  // reserved damage action, then buffered cancel (F:212-229).  Written as a value
-  // select so the compiler cannot merge the two tails into a pointer phi (which
-  // would pin the whole arena in scratch memory).
+  // reserved damage action, then buffered cancel: SetCurrentAction and return (F:212-229)
   const int rsv = f.rsv, buf = f.buf;
   const bool take_rsv = rsv != NONE && f.stun <= 0;
   const bool take_buf = !take_rsv && buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0;
-  if (take_rsv || take_buf) {
-    set_action(f, take_rsv ? rsv : buf);
-    return;
-  }
-  if (e.special) {
-    request_action(f, (e.fwd || e.back) ? A_B_SPECIAL : A_N_SPECIAL);
-  } else if (e.atk_down) {
-    if ((f.act == A_N_ATTACK || f.act == A_B_ATTACK) && f.frame < sT.action[f.act].frame_count)
-      request_action(f, A_N_SPECIAL);
-    else
-      request_action(f, (e.fwd || e.back) ? A_B_ATTACK : A_N_ATTACK);
-  }
-  if (e.fdash) request_action(f, A_DASH_FORWARD);
-  else if (e.bdash) request_action(f, A_DASH_BACKWARD);
-  f.in_back = e.back;
-  if (e.fwd && e.back) request_action(f, A_STAND);
-  else if (e.fwd) request_action(f, A_FORWARD);
-  else if (e.back) request_action(f, f.prox ? A_GUARD_PROXIMITY : A_BACKWARD);
-  else request_action(f, A_STAND);
-  f.prox = false;
+  const bool early = take_rsv | take_buf;
+  const int a0 = take_rsv ? rsv : buf;
+  // special / attack (F:234-254), dash (F:256-259), movement (F:265-283)
+  const bool dir = e.fwd | e.back;
+  const bool in_normal = (f.act == A_N_ATTACK || f.act == A_B_ATTACK) && f.frame < ai_frame_count(ai);
+  const int a1 = e.special ? (dir ? A_B_SPECIAL : A_N_SPECIAL)
+                           : (in_normal ? A_N_SPECIAL : (dir ? A_B_ATTACK : A_N_ATTACK));
+  const int a2 = e.fdash ? A_DASH_FORWARD : A_DASH_BACKWARD;
+  const int a3 = (e.fwd & e.back) ? A_STAND
+                 : e.fwd          ? A_FORWARD
+                 : e.back         ? (f.prox ? A_GUARD_PROXIMITY : A_BACKWARD)
+                                  : A_STAND;
+  const AInfo i1 = action_info(a1), i2 = action_info(a2), i3 = action_info(a3);
+  f.act = early ? a0 : f.act;
+  f.frame = early ? 0 : f.frame;
+  f.hits = early ? 0 : f.hits;
+  f.buf = early ? NONE : f.buf;
+  f.rsv = early ? NONE : f.rsv;
+  request_action(f, ai, a1, i1, !early & (e.special | e.atk_down));
+  request_action(f, ai, a2, i2, !early & (e.fdash | e.bdash));
+  request_action(f, ai, a3, i3, !early);
+  f.in_back = early ? f.in_back : e.back;  // for proximity guard (F:263)
+  f.prox = early ? f.prox : false;         // F:285
 }
 
+// UpdateMovement (F:291-319).  FORWARD / BACKWARD walk at the fighter speeds; any
+// other action takes the first movement window's velocity (0 = none).  BACKWARD's
+// `pos -= s*sign*dt` is `pos + (-s)*sign*dt` bit for bit (negation is exact and
+// round-to-nearest is symmetric), so one expression covers all three.
 template <int FM>
-__device__ __forceinline__ void update_movement(Fighter& f, float sign) {
-  if (f.stun > 0) return;
-  if (f.act == A_FORWARD) {
-    f.x = pos_plus_vel<FM>(f.x, kForwardSpeed, sign);
-  } else if (f.act == A_BACKWARD) {
-    f.x = pos_minus_vel<FM>(f.x, kBackwardSpeed, sign);
-  } else {
-    const uint32_t vi = sT.rows[sT.action[f.act].row + f.frame] & 15;
-    if (vi) {
-      const float v = sT.vels[vi];
-      if (v != 0.0f) f.x = pos_plus_vel<FM>(f.x, v, sign);
-    }
-  }
+__device__ __forceinline__ void update_movement(Fighter& f, float sign, float rec_vel) {
+  const float v = f.act == A_FORWARD ? kForwardSpeed : f.act == A_BACKWARD ? -kBackwardSpeed : rec_vel;
+  const float nx = pos_plus_vel<FM>(f.x, v, sign);
+  f.x = (f.stun <= 0 && v != 0.0f) ? nx : f.x;
 }
 
+// the frame record of (act, frame) after the action request
+__device__ __forceinline__ int frame_record(const Fighter& f) {
+  return sT.rec_index[f.act * kFrameStride + min(f.frame, kFrameStride - 1)];
+}
+
+// UpdateBoxes (F:671-697): world x of every box of the record
 template <int FM>
-__device__ __forceinline__ void update_boxes(Fighter& f, float sign) {
-  const uint32_t row = sT.rows[sT.action[f.act].row + f.frame];
-  f.push_rect = (row >> 4) & 31;
-  f.hurtset = sT.hurtsets[(row >> 9) & 63];
-  f.hitset = sT.hitsets[(row >> 15) & 63];
-  f.px = xform<FM>(f.x, sT.rects[f.push_rect].x, sign);
-  f.ux0 = xform<FM>(f.x, sT.rects[(f.hurtset >> 2) & 63].x, sign);
-  f.ux1 = xform<FM>(f.x, sT.rects[(f.hurtset >> 8) & 63].x, sign);
-  f.hx0 = xform<FM>(f.x, sT.rects[(f.hitset >> 2) & 63].x, sign);
-  f.hx1 = xform<FM>(f.x, sT.rects[(f.hitset >> 11) & 63].x, sign);
+__device__ __forceinline__ void update_boxes(Fighter& f, float sign, const FrameRec& R) {
+  f.info = R.info;
+  f.px = xform<FM>(f.x, R.push.x, sign);
+  f.ux0 = xform<FM>(f.x, R.hurt[0].x, sign);
+  f.ux1 = xform<FM>(f.x, R.hurt[1].x, sign);
+  f.hx0 = xform<FM>(f.x, R.hit[0].x, sign);
+  f.hx1 = xform<FM>(f.x, R.hit[1].x, sign);
 }
 
 // ApplyPositionChange (F:331-350): position and every box are shifted, not rebuilt
@@ -381,48 +405,10 @@ __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
   f.hx1 = fadd<FM>(f.hx1, dx);
 }
 
-// UpdatePushCharacterVsCharacter (BC:483-501) with UnityEngine.Rect semantics:
-// x is xMin, xMax = width + x, Overlaps is strict.
-template <int FM>
-__device__ __forceinline__ void push_character_vs_character(Fighter& a, Fighter& b) {
-  const float4 ra = sT.rects[a.push_rect], rb = sT.rects[b.push_rect];
-  const float a_xmax = fadd<FM>(ra.z, a.px), b_xmax = fadd<FM>(rb.z, b.px);
-  const float a_ymax = fadd<FM>(ra.w, ra.y), b_ymax = fadd<FM>(rb.w, rb.y);
-  const bool overlap = b_xmax > a.px && b.px < a_xmax && b_ymax > ra.y && rb.y < a_ymax;
-  if (!overlap) return;
-  if (a.x < b.x) {
-    float da, db;
-    if constexpr (FM == FS_FLOAT_DOUBLE) {
-      const double d = (double)a_xmax - (double)b.px;
-      da = (float)(d * -1 / 2);
-      db = (float)(d * 1 / 2);
-    } else {
-      const float d = __fsub_rn(a_xmax, b.px);
-      da = d * -1.0f / 2.0f;
-      db = d * 1.0f / 2.0f;
-    }
-    apply_position_change<FM>(a, da);
-    apply_position_change<FM>(b, db);
-  } else if (a.x > b.x) {
-    float da, db;
-    if constexpr (FM == FS_FLOAT_DOUBLE) {
-      const double d = (double)b_xmax - (double)a.px;
-      da = (float)(d * 1 / 2);
-      db = (float)(d * -1 / 2);
-    } else {
-      const float d = __fsub_rn(b_xmax, a.px);
-      da = d * 1.0f / 2.0f;
-      db = d * -1.0f / 2.0f;
-    }
-    apply_position_change<FM>(a, da);
-    apply_position_change<FM>(b, db);
-  }
-}
-
 // UpdatePushCharacterVsBackground (BC:503-519) with BoxBase semantics
 template <int FM>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
-  const float w = sT.rects[f.push_rect].z;
+  const float w = sT.recs[f.rec].push.z;
   const float xmin = bb_xmin<FM>(f.px, w);
   if (xmin < -kStageHalf) {
     apply_position_change<FM>(f, fsub<FM>(-kStageHalf, xmin));
@@ -470,41 +456,36 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
   return DR_DAMAGE;
 }
 
-// The box test of one attacker of UpdateHitboxHurtboxCollision (BC:535-569):
-// attacker hitboxes in order, skipping attacks that already hit (CanAttackHit,
+// The box test of one attacker of UpdateHitboxHurtboxCollision (BC:535-569): the
+// attacker's hitboxes in order, skipping attacks that already hit (CanAttackHit,
 // F:408-420); a proximity box only flags proximity, a real box is a hit and ends
-// the scan.
+// the scan.  Evaluated branch-free over the 2x2 box pairs: the hit's attack is the
+// first real box that overlaps, and proximity only matters when nothing hit.
 struct HitTest {
   bool hit, prox;
   int atk;
 };
 
 template <int FM>
-__device__ __forceinline__ HitTest hit_test(uint32_t hitset, float hx0, float hx1, int hits, uint32_t hurtset,
-                                            float ux0, float ux1) {
-  HitTest t{false, false, 0};
-  const int nh = hitset & 3, nu = hurtset & 3;
-  for (int h = 0; h < nh; h++) {
-    const uint32_t hb = (hitset >> (2 + 9 * h)) & 511;
-    const int aidx = (hb >> 6) & 3;
-    if (hits >= sT.attacks[aidx].number_of_hit) continue;
-    const float4 hr = sT.rects[hb & 63];
-    const float hx = h == 0 ? hx0 : hx1;
-    for (int u = 0; u < nu; u++) {
-      const float4 ur = sT.rects[(hurtset >> (2 + 6 * u)) & 63];
-      const float ux = u == 0 ? ux0 : ux1;
-      if (box_overlaps<FM>(hx, hr, ux, ur)) {
-        if ((hb >> 8) & 1) {
-          t.prox = true;
-        } else {
-          t.hit = true;
-          t.atk = aidx;
-          break;
-        }
-      }
-    }
-    if (t.hit) break;
-  }
+__device__ __forceinline__ HitTest hit_test(uint32_t att_info, float4 h0, float4 h1, float hx0, float hx1,
+                                            int att_hits, uint32_t def_info, float4 u0, float4 u1, float ux0,
+                                            float ux1) {
+  const int nh = (att_info >> 2) & 3, nu = def_info & 3;
+  const uint32_t b0 = (att_info >> 4) & 31, b1 = (att_info >> 9) & 31;  // atk 2b | prox 1b | numberOfHit 2b
+  const bool c0 = (nh > 0) & (att_hits < (int)(b0 >> 3));
+  const bool c1 = (nh > 1) & (att_hits < (int)(b1 >> 3));
+  const bool v0 = nu > 0, v1 = nu > 1;
+  const bool o00 = c0 & v0 & box_overlaps<FM>(hx0, h0, ux0, u0);
+  const bool o01 = c0 & v1 & box_overlaps<FM>(hx0, h0, ux1, u1);
+  const bool o10 = c1 & v0 & box_overlaps<FM>(hx1, h1, ux0, u0);
+  const bool o11 = c1 & v1 & box_overlaps<FM>(hx1, h1, ux1, u1);
+  const bool any0 = o00 | o01, any1 = o10 | o11;
+  const bool p0 = (b0 >> 2) & 1, p1 = (b1 >> 2) & 1;
+  const bool hit0 = any0 & !p0, hit1 = any1 & !p1;
+  HitTest t;
+  t.hit = hit0 | hit1;
+  t.atk = hit0 ? (int)(b0 & 3) : (int)(b1 & 3);
+  t.prox = (any0 & p0) | (any1 & p1);
   return t;
 }
 
@@ -731,10 +712,10 @@ __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int
 template <int FM>
 __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t k) {
   const float o_px = xpair(f.px), o_x = xpair(f.x);
-  const int o_rect = xpair(f.push_rect);
+  const int o_rec = xpair(f.rec);
   const float px1 = k == 0 ? f.px : o_px, px2 = k == 0 ? o_px : f.px;
   const float x1 = k == 0 ? f.x : o_x, x2 = k == 0 ? o_x : f.x;
-  const float4 r1 = sT.rects[k == 0 ? f.push_rect : o_rect], r2 = sT.rects[k == 0 ? o_rect : f.push_rect];
+  const float4 r1 = sT.recs[k == 0 ? f.rec : o_rec].push, r2 = sT.recs[k == 0 ? o_rec : f.rec].push;
   const float xmax1 = fadd<FM>(r1.z, px1), xmax2 = fadd<FM>(r2.z, px2);
   const float ymax1 = fadd<FM>(r1.w, r1.y), ymax2 = fadd<FM>(r2.w, r2.y);
   const bool overlap = xmax2 > px1 && px2 < xmax1 && ymax2 > r1.y && r2.y < ymax1;
@@ -759,21 +740,28 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
 // NotifyDamaged, the attacker lane NotifyAttackHit, and both take the stun.
 template <int FM>
 __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k) {
-  const uint32_t o_hitset = xpair(f.hitset), o_hurtset = xpair(f.hurtset);
+  const uint32_t o_info = xpair(f.info);
+  if ((((f.info | o_info) >> 2) & 3) == 0) return;  // only attack actions carry hitboxes
+  const int o_rec = xpair(f.rec);
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1), o_ux0 = xpair(f.ux0), o_ux1 = xpair(f.ux1);
-  if (((f.hitset | o_hitset) & 3) == 0) return;  // only attack actions carry hitboxes
+  const FrameRec& mine = sT.recs[f.rec];
+  const FrameRec& theirs = sT.recs[o_rec];
+  const float4 my_h0 = mine.hit[0], my_h1 = mine.hit[1], my_u0 = mine.hurt[0], my_u1 = mine.hurt[1];
+  const float4 o_h0 = theirs.hit[0], o_h1 = theirs.hit[1], o_u0 = theirs.hurt[0], o_u1 = theirs.hurt[1];
 #pragma unroll
   for (uint32_t phase = 0; phase < 2; phase++) {
     const bool attacking = k == phase;
     const int o_hits = xpair(f.hits);
-    const HitTest t = attacking ? hit_test<FM>(f.hitset, f.hx0, f.hx1, f.hits, o_hurtset, o_ux0, o_ux1)
-                                : hit_test<FM>(o_hitset, o_hx0, o_hx1, o_hits, f.hurtset, f.ux0, f.ux1);
+    const HitTest t = hit_test<FM>(attacking ? f.info : o_info, attacking ? my_h0 : o_h0, attacking ? my_h1 : o_h1,
+                                   attacking ? f.hx0 : o_hx0, attacking ? f.hx1 : o_hx1, attacking ? f.hits : o_hits,
+                                   attacking ? o_info : f.info, attacking ? o_u0 : my_u0, attacking ? o_u1 : my_u1,
+                                   attacking ? o_ux0 : f.ux0, attacking ? o_ux1 : f.ux1);
     int stun = 0;
     if (t.hit) {
-      const AttackInfo ad = sT.attacks[t.atk];
       if (attacking) {
         f.hits++;  // NotifyAttackHit (F:352-355)
       } else {
+        const AttackInfo ad = sT.attacks[t.atk];
         const int res = notify_damaged(f, ad);
         stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
       }
@@ -922,10 +910,13 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   }
   const float sign = k == 0 ? 1.0f : -1.0f;
   const InputEval e = update_input(L.f, L.act, (int)k);
-  increment_action_frame(L.f);
-  update_action_request(L.f, e);
-  update_movement<FM>(L.f, sign);
-  update_boxes<FM>(L.f, sign);
+  AInfo ai = action_info(L.f.act);
+  increment_action_frame(L.f, ai);
+  update_action_request(L.f, e, ai);
+  L.f.rec = frame_record(L.f);
+  const FrameRec& R = sT.recs[L.f.rec];
+  update_movement<FM>(L.f, sign, R.vel);
+  update_boxes<FM>(L.f, sign, R);
   push_character_vs_character<FM>(L.f, k);
   push_character_vs_background<FM>(L.f);
   hitbox_hurtbox_collision<FM>(L.f, k);
@@ -1032,6 +1023,10 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
     load_lane<BOT>(L, p.st, a, k);
   }
   if (p.seeds) L.bot.rng = rng_init((int32_t)(uint32_t)p.seeds[a]);  // SEED (BC:170-173)
+  if (p.flags == FS_RESET_SEED_ONLY) {
+    store_lane<BOT>(L, p.st, a);
+    return;
+  }
   const bool hard = p.init || p.flags == FS_RESET_HARD || !L.has_term;
   if (L.pending) {  // finish the burst Unity ran after the terminal frame
     reset_burst<FM, BOT>(L, true);

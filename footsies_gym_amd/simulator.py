@@ -105,12 +105,13 @@ class FootsiesSim:
         check(lib().fs_set_stream(self._h, C.c_void_p(s.cuda_stream)), self._h)
 
     # -- core API --------------------------------------------------------------------
-    def reset(self, seeds=None, mask=None, hard=False):
-        """FootsiesEnv.reset over all (or the masked) arenas; seeds -> Random.InitState."""
+    def reset(self, seeds=None, mask=None, hard=False, seed_only=False):
+        """FootsiesEnv.reset over all (or the masked) arenas; seeds -> Random.InitState.
+        seed_only: the SEED command alone (no reset, outputs untouched)."""
         n = self.num_envs
         s = None if seeds is None else np.ascontiguousarray(np.broadcast_to(np.asarray(seeds, dtype=np.uint64), (n,)))
         m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(n))
-        flags = _abi.FS_RESET_HARD if hard else _abi.FS_RESET_IF_NEEDED
+        flags = _abi.FS_RESET_SEED_ONLY if seed_only else (_abi.FS_RESET_HARD if hard else _abi.FS_RESET_IF_NEEDED)
         check(lib().fs_reset(self._h, None if s is None else s.ctypes.data, None if m is None else m.ctypes.data,
                              flags), self._h)
         return self._out

@@ -61,6 +61,8 @@ extern "C" {
 #define FS_RESET_IF_NEEDED 1    /* FootsiesEnv.reset (FE:482-515): RESET only arenas whose
                                    has_terminated flag is clear; the others just finish the
                                    pending KO->...->Fight burst (if any) and report state(-1) */
+#define FS_RESET_SEED_ONLY 2    /* SEED command alone (BC:170-173): Random.InitState on the masked
+                                   arenas, nothing else changes and no outputs are written */
 
 typedef struct fs_config {
   int32_t num_envs;        /* arenas on this handle (>0) */

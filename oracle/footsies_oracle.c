@@ -1152,6 +1152,10 @@ OR_EXPORT int or_reset(or_handle C, const uint64_t* seeds, const uint8_t* mask, 
 #pragma omp parallel for schedule(static) if (C->n >= 1024)
   for (int i = 0; i < C->n; i++) {
     if (mask && !mask[i]) continue;
+    if (flags == FS_RESET_SEED_ONLY) { /* SEED alone (BC:170-173) */
+      if (seeds) rng_init(C->a[i].rng, (int32_t)(uint32_t)seeds[i]);
+      continue;
+    }
     int hard = (flags == FS_RESET_HARD) || !C->a[i].has_terminated;
     fe_reset_arena(C, i, seeds, hard);
   }

@@ -70,9 +70,12 @@ def test_resets_lockstep(oracle_lib):
         mask = (rng.random(256) < 0.5).astype(np.uint8)
         seeds = rng.integers(0, 2**31, 256).astype(np.uint64) if rnd % 2 else None
         hard = rnd % 3 == 0
-        flags = _abi.FS_RESET_HARD if hard else _abi.FS_RESET_IF_NEEDED
+        seed_only = rnd == 4
+        flags = (_abi.FS_RESET_SEED_ONLY if seed_only else _abi.FS_RESET_HARD if hard else _abi.FS_RESET_IF_NEEDED)
+        if seed_only:
+            seeds = rng.integers(0, 2**31, 256).astype(np.uint64)
         eo = ora.reset(seeds=seeds, mask=mask, flags=flags)
-        sim.reset(seeds=seeds, mask=mask, hard=hard)
+        sim.reset(seeds=seeds, mask=mask, hard=hard, seed_only=seed_only)
         compare_outputs(eo, sim.outputs_numpy(), step=-2)
         compare_states(ora.state(), sim.get_state(), step=-2)
 
