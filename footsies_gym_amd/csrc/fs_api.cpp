@@ -305,6 +305,9 @@ FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p
                      const fs_outputs* traj) {
   if (!h) return FS_E_INVALID;
   if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n: n must be > 0");
+  // the kernels index actions and trajectory rows with 32-bit offsets ([n][N][2] elements)
+  if ((uint64_t)n * (uint64_t)h->n * 2u > 0x7fffffffull)
+    return set_err(h, FS_E_INVALID, "fs_step_n: n * num_envs too large for one launch; split it");
   if ((p1_act == nullptr) != (p2_act == nullptr) && h->cfg.p2_mode == FS_P2_EXTERNAL)
     return set_err(h, FS_E_INVALID, "fs_step_n: give both action arrays or neither");
   return step_common(h, n, p1_act, p2_act, FS_ACT_DEVICE, action_seed, traj);

@@ -408,7 +408,7 @@ __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
 // UpdatePushCharacterVsBackground (BC:503-519) with BoxBase semantics
 template <int FM>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
-  const float w = sT.recs[f.rec].push.z;
+  const float w = sT.recs[f.rec].push.y;
   const float xmin = bb_xmin<FM>(f.px, w);
   if (xmin < -kStageHalf) {
     apply_position_change<FM>(f, fsub<FM>(-kStageHalf, xmin));
@@ -418,14 +418,15 @@ __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
   }
 }
 
-// BoxBase.Overlaps (F:17-25), inclusive; `self` is the hitbox, `other` the hurtbox
+// BoxBase.Overlaps (F:17-25), inclusive; `self` is the hitbox, `other` the hurtbox.
+// Boxes are (world x, width/2, yMin, yMax): xMin = x - w/2, xMax = x + w/2 (F:12-13).
 template <int FM>
 __device__ __forceinline__ bool box_overlaps(float sx, float4 sr, float ox, float4 orr) {
-  const bool c1 = bb_xmax<FM>(ox, orr.z) >= bb_xmin<FM>(sx, sr.z);
-  const bool c2 = bb_xmin<FM>(ox, orr.z) <= bb_xmax<FM>(sx, sr.z);
-  const bool c3 = fadd<FM>(orr.y, orr.w) >= sr.y;
-  const bool c4 = orr.y <= fadd<FM>(sr.y, sr.w);
-  return c1 && c2 && c3 && c4;
+  const bool c1 = fadd<FM>(ox, orr.y) >= fsub<FM>(sx, sr.y);
+  const bool c2 = fsub<FM>(ox, orr.y) <= fadd<FM>(sx, sr.y);
+  const bool c3 = orr.w >= sr.z;
+  const bool c4 = orr.z <= sr.w;
+  return c1 & c2 & c3 & c4;
 }
 
 constexpr int DR_DAMAGE = 1, DR_GUARD = 2, DR_GUARD_BREAK = 3;
@@ -459,32 +460,41 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
 // The box test of one attacker of UpdateHitboxHurtboxCollision (BC:535-569): the
 // attacker's hitboxes in order, skipping attacks that already hit (CanAttackHit,
 // F:408-420); a proximity box only flags proximity, a real box is a hit and ends
-// the scan.  Evaluated branch-free over the 2x2 box pairs: the hit's attack is the
-// first real box that overlaps, and proximity only matters when nothing hit.
+// the scan.  Branch-free over the 2x2 box pairs: the hit's attack is the first real
+// box that overlaps, and proximity only matters when nothing hit.  The overlaps do
+// not depend on the attacker's hit count, so they are computed once (`BoxHits`) and
+// resolved for a given hit count by `resolve`.
 struct HitTest {
   bool hit, prox;
   int atk;
 };
 
+struct BoxHits {
+  bool any0, any1;  // hitbox j overlaps some defender hurtbox
+  uint32_t b0, b1;  // hitbox j bits: attack idx 2b | proximity 1b | numberOfHit 2b
+};
+
 template <int FM>
-__device__ __forceinline__ HitTest hit_test(uint32_t att_info, float4 h0, float4 h1, float hx0, float hx1,
-                                            int att_hits, uint32_t def_info, float4 u0, float4 u1, float ux0,
-                                            float ux1) {
+__device__ __forceinline__ BoxHits box_hits(uint32_t att_info, float4 h0, float4 h1, float hx0, float hx1,
+                                            uint32_t def_info, float4 u0, float4 u1, float ux0, float ux1) {
   const int nh = (att_info >> 2) & 3, nu = def_info & 3;
-  const uint32_t b0 = (att_info >> 4) & 31, b1 = (att_info >> 9) & 31;  // atk 2b | prox 1b | numberOfHit 2b
-  const bool c0 = (nh > 0) & (att_hits < (int)(b0 >> 3));
-  const bool c1 = (nh > 1) & (att_hits < (int)(b1 >> 3));
   const bool v0 = nu > 0, v1 = nu > 1;
-  const bool o00 = c0 & v0 & box_overlaps<FM>(hx0, h0, ux0, u0);
-  const bool o01 = c0 & v1 & box_overlaps<FM>(hx0, h0, ux1, u1);
-  const bool o10 = c1 & v0 & box_overlaps<FM>(hx1, h1, ux0, u0);
-  const bool o11 = c1 & v1 & box_overlaps<FM>(hx1, h1, ux1, u1);
-  const bool any0 = o00 | o01, any1 = o10 | o11;
-  const bool p0 = (b0 >> 2) & 1, p1 = (b1 >> 2) & 1;
+  BoxHits r;
+  r.b0 = (att_info >> 4) & 31;
+  r.b1 = (att_info >> 9) & 31;
+  r.any0 = (nh > 0) & ((v0 & box_overlaps<FM>(hx0, h0, ux0, u0)) | (v1 & box_overlaps<FM>(hx0, h0, ux1, u1)));
+  r.any1 = (nh > 1) & ((v0 & box_overlaps<FM>(hx1, h1, ux0, u0)) | (v1 & box_overlaps<FM>(hx1, h1, ux1, u1)));
+  return r;
+}
+
+__device__ __forceinline__ HitTest resolve(const BoxHits& r, int att_hits) {
+  const bool any0 = r.any0 & (att_hits < (int)(r.b0 >> 3));  // CanAttackHit
+  const bool any1 = r.any1 & (att_hits < (int)(r.b1 >> 3));
+  const bool p0 = (r.b0 >> 2) & 1, p1 = (r.b1 >> 2) & 1;
   const bool hit0 = any0 & !p0, hit1 = any1 & !p1;
   HitTest t;
   t.hit = hit0 | hit1;
-  t.atk = hit0 ? (int)(b0 & 3) : (int)(b1 & 3);
+  t.atk = hit0 ? (int)(r.b0 & 3) : (int)(r.b1 & 3);
   t.prox = (any0 & p0) | (any1 & p1);
   return t;
 }
@@ -715,10 +725,10 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
   const int o_rec = xpair(f.rec);
   const float px1 = k == 0 ? f.px : o_px, px2 = k == 0 ? o_px : f.px;
   const float x1 = k == 0 ? f.x : o_x, x2 = k == 0 ? o_x : f.x;
+  // record pushboxes are (x offset, width, yMin, yMax); position.y == 0
   const float4 r1 = sT.recs[k == 0 ? f.rec : o_rec].push, r2 = sT.recs[k == 0 ? o_rec : f.rec].push;
-  const float xmax1 = fadd<FM>(r1.z, px1), xmax2 = fadd<FM>(r2.z, px2);
-  const float ymax1 = fadd<FM>(r1.w, r1.y), ymax2 = fadd<FM>(r2.w, r2.y);
-  const bool overlap = xmax2 > px1 && px2 < xmax1 && ymax2 > r1.y && r2.y < ymax1;
+  const float xmax1 = fadd<FM>(r1.y, px1), xmax2 = fadd<FM>(r2.y, px2);
+  const bool overlap = (xmax2 > px1) & (px2 < xmax1) & (r2.w > r1.z) & (r2.z < r1.w);
   if (!overlap || x1 == x2) return;  // a tie pushes nothing (BC:490-499)
   float d1, d2;  // shifts of P1, P2
   if constexpr (FM == FS_FLOAT_DOUBLE) {
@@ -733,43 +743,52 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
   apply_position_change<FM>(f, k == 0 ? d1 : d2);
 }
 
-// UpdateHitboxHurtboxCollision (BC:521-591): attacker P1 then attacker P2.  The
-// boxes are those of UpdateBoxes (not rebuilt when a hit changes the action), but
-// the hit count is re-read: P2's may have been reset by P1's hit (sequential trade
-// semantics).  Both lanes run the same box test; the defender lane applies
-// NotifyDamaged, the attacker lane NotifyAttackHit, and both take the stun.
+// UpdateHitboxHurtboxCollision (BC:521-591): attacker P1 (phase A), then attacker P2
+// (phase B).  The boxes are those of UpdateBoxes (not rebuilt when a hit changes an
+// action), but phase B re-reads P2's hit count, which phase A resets if it hit P2
+// (sequential trade semantics).  Each lane tests the partner's hitboxes against its
+// own hurtboxes in one pass -- the P2 lane is phase A's defender, the P1 lane phase
+// B's -- and phase B is resolved for both possible P2 hit counts, so only the
+// outcomes cross the pair: A's result to P1 (NotifyAttackHit), whether P2 was hit to
+// P1 (to pick B's variant), B's result to P2, and each defender's stun to the other.
 template <int FM>
 __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k) {
   const uint32_t o_info = xpair(f.info);
   if ((((f.info | o_info) >> 2) & 3) == 0) return;  // only attack actions carry hitboxes
   const int o_rec = xpair(f.rec);
-  const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1), o_ux0 = xpair(f.ux0), o_ux1 = xpair(f.ux1);
+  const int o_hits = xpair(f.hits);
+  const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
   const FrameRec& mine = sT.recs[f.rec];
   const FrameRec& theirs = sT.recs[o_rec];
-  const float4 my_h0 = mine.hit[0], my_h1 = mine.hit[1], my_u0 = mine.hurt[0], my_u1 = mine.hurt[1];
-  const float4 o_h0 = theirs.hit[0], o_h1 = theirs.hit[1], o_u0 = theirs.hurt[0], o_u1 = theirs.hurt[1];
-#pragma unroll
-  for (uint32_t phase = 0; phase < 2; phase++) {
-    const bool attacking = k == phase;
-    const int o_hits = xpair(f.hits);
-    const HitTest t = hit_test<FM>(attacking ? f.info : o_info, attacking ? my_h0 : o_h0, attacking ? my_h1 : o_h1,
-                                   attacking ? f.hx0 : o_hx0, attacking ? f.hx1 : o_hx1, attacking ? f.hits : o_hits,
-                                   attacking ? o_info : f.info, attacking ? o_u0 : my_u0, attacking ? o_u1 : my_u1,
-                                   attacking ? o_ux0 : f.ux0, attacking ? o_ux1 : f.ux1);
-    int stun = 0;
-    if (t.hit) {
-      if (attacking) {
-        f.hits++;  // NotifyAttackHit (F:352-355)
-      } else {
-        const AttackInfo ad = sT.attacks[t.atk];
-        const int res = notify_damaged(f, ad);
-        stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
-      }
-    }
-    const int o_stun = xpair(stun);
-    if (t.hit) f.stun = attacking ? o_stun : stun;  // SetHitStun on both (BC:576-578)
-    else if (t.prox && !attacking && f.in_back) f.prox = true;  // NotifyInProximityGuardRange (F:400-406)
+  const BoxHits bh = box_hits<FM>(o_info, theirs.hit[0], theirs.hit[1], o_hx0, o_hx1, f.info, mine.hurt[0],
+                                  mine.hurt[1], f.ux0, f.ux1);
+  // phase A on the P2 lane: P1 attacks P2
+  HitTest tA = resolve(bh, o_hits);
+  int stunA = 0;
+  if (k == 1 && tA.hit) {
+    const AttackInfo ad = sT.attacks[tA.atk];
+    const int res = notify_damaged(f, ad);
+    stunA = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
   }
+  if (k == 1 && !tA.hit && tA.prox && f.in_back) f.prox = true;  // NotifyInProximityGuardRange (F:400-406)
+  const uint32_t a_bits = xpair((uint32_t)tA.hit | ((uint32_t)stunA << 1));
+  const bool hitA = k == 1 ? tA.hit : (a_bits & 1);
+  stunA = k == 1 ? stunA : (int)(a_bits >> 1);
+  if (k == 0 && hitA) f.hits++;  // NotifyAttackHit for P1 (F:352-355)
+  // phase B on the P1 lane: P2 attacks P1 with its hit count after phase A
+  HitTest tB = resolve(bh, hitA ? 0 : o_hits);
+  int stunB = 0;
+  if (k == 0 && tB.hit) {
+    const AttackInfo ad = sT.attacks[tB.atk];
+    const int res = notify_damaged(f, ad);
+    stunB = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
+  }
+  if (k == 0 && !tB.hit && tB.prox && f.in_back) f.prox = true;
+  const uint32_t b_bits = xpair((uint32_t)tB.hit | ((uint32_t)stunB << 1));
+  const bool hitB = k == 0 ? tB.hit : (b_bits & 1);
+  stunB = k == 0 ? stunB : (int)(b_bits >> 1);
+  if (k == 1 && hitB) f.hits++;  // NotifyAttackHit for P2
+  f.stun = hitB ? stunB : (hitA ? stunA : f.stun);  // SetHitStun on both, phase B last (BC:576-578)
 }
 
 // KO tick -> End (winner), End tick (BC:221-243, 306-325, 371-381), reduced to
@@ -845,11 +864,11 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void write_obs(const Lane& L, uint8_t* guard, uint8_t* move, float* move_frame,
                                           float* position, int32_t* frame, uint8_t* action, uint8_t* hitstun,
-                                          size_t r) {
+                                          uint32_t r) {
   int a = L.f.act;
   if (a == A_DEAD || a == A_WIN) a = A_STAND;  // FE:537-549
   const int mf = (a == A_STAND || a == A_FORWARD || a == A_BACKWARD) ? 0 : L.f.frame;  // FE:339-358
-  const size_t c = 2 * r + L.k;
+  const uint32_t c = 2 * r + L.k;
   guard[c] = (uint8_t)L.f.guard;
   move[c] = (uint8_t)a;
   move_frame[c] = (float)mf;
@@ -859,10 +878,10 @@ __device__ __forceinline__ void write_obs(const Lane& L, uint8_t* guard, uint8_t
   if (L.k == 0) frame[r] = L.frame_count;
 }
 
-__device__ __forceinline__ void write_main(const Lane& L, const DevOutputs& o, size_t r) {
+__device__ __forceinline__ void write_main(const Lane& L, const DevOutputs& o, uint32_t r) {
   write_obs(L, o.guard, o.move, o.move_frame, o.position, o.frame, o.action, o.hitstun, r);
 }
-__device__ __forceinline__ void write_final(const Lane& L, const DevOutputs& o, size_t r) {
+__device__ __forceinline__ void write_final(const Lane& L, const DevOutputs& o, uint32_t r) {
   write_obs(L, o.final_guard, o.final_move, o.final_move_frame, o.final_position, o.final_frame, o.final_action,
             o.final_hitstun, r);
 }
@@ -882,7 +901,7 @@ __device__ __forceinline__ uint32_t hash_action(uint64_t seed, uint64_t env, uin
 // (BC:201-220, 347-364) and, for a terminal arena, the auto-reset burst
 // ---------------------------------------------------------------------------
 template <int FM, int P2>
-__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, size_t r) {
+__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   const DevOutputs& o = p.out;
   const uint32_t k = L.k;
@@ -967,13 +986,10 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step(StepParams p) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  stage_tables();
-  if (l >= 2 * p.n_envs) return;
   constexpr bool BOT = P2 == FS_P2_BOT;
-  const int a = l >> 1;
+  const bool active = l < 2 * p.n_envs;
+  const int a = active ? l >> 1 : 0;
   const uint32_t k = l & 1;
-  Lane L;
-  load_lane<BOT>(L, p.st, a, k);
   // This lane's action, software-pipelined one tick ahead: the load for tick t+1
   // is issued before tick t's output stores, so its wait does not drain them
   // (loads and stores retire in order on one vmcnt counter).
@@ -981,13 +997,20 @@ __global__ __launch_bounds__(256) void k_step(StepParams p) {
   const bool reads = k == 0 || P2 == FS_P2_EXTERNAL;
   auto fetch = [&](int t) -> uint32_t {
     if (!reads) return 0u;
-    return src ? src[(size_t)t * p.n_envs + a] : hash_action(p.action_seed, a, p.t0 + (uint64_t)t, k);
+    return src ? src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a]
+               : hash_action(p.action_seed, a, p.t0 + (uint64_t)t, k);
   };
+  // the arena state and the first action are in flight while the block stages the tables
+  Lane L;
+  load_lane<BOT>(L, p.st, a, k);
   uint32_t next = fetch(0);
+  stage_tables();
+  if (!active) return;
+  const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
   for (int t = 0; t < p.n_steps; t++) {
     const uint32_t act = next;
     if (t + 1 < p.n_steps) next = fetch(t + 1);
-    env_step<FM, P2>(L, act & 7u, p, (size_t)t * p.out_stride_steps * p.n_envs + a);
+    env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a);
   }
   store_lane<BOT>(L, p.st, a);
 }
