@@ -61,7 +61,7 @@ def cpu_baseline(envs, seconds, seed):
     t = time.perf_counter()
     o.step_n_hashed(10, seed)
     probe = time.perf_counter() - t
-    steps = int(max(10, min(5000, seconds / max(probe / 10, 1e-9))))
+    steps = int(max(10, min(200000, seconds / max(probe / 10, 1e-9))))
     t = time.perf_counter()
     o.step_n_hashed(steps, seed)
     dt = time.perf_counter() - t
@@ -69,6 +69,23 @@ def cpu_baseline(envs, seconds, seed):
     return {"value": envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": "%d arenas x %d steps, self-play splitmix64 actions, oracle/liboracle.so (OpenMP %d threads), "
                       "%.1f s" % (envs, steps, threads, dt)}
+
+
+def pmc_traffic(kernel, envs, ticks):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/*_traffic.json, written by tools/summarize_profile.py from separate
+    FETCH_SIZE / WRITE_SIZE passes over this same bench command): FETCH_SIZE x 2
+    (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, KiB -> bytes.
+    None when no summary for this kernel at this arena count / ticks per launch."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        with open(path) as f:
+            doc = json.load(f)
+        for k in doc.get("kernels", []):
+            if k["kernel"] == kernel and k["envs"] == envs and k["ticks_per_launch"] == ticks:
+                best = (k["traffic_bytes_per_launch"], os.path.relpath(path, ROOT))
+    return best
 
 
 def main():
@@ -164,6 +181,19 @@ def main():
         wall, ev = timed(fn, W, K)
         res[mode] = {"wall_s": wall, "event_s": ev, "env_steps_per_s": world * N * K / wall,
                      "ms_per_step": 1e3 * wall / K}
+    # P1/P2 actions handed over from host memory (FS_ACT_HOST: pinned staging + H2D copy per
+    # step), the PCIe-inclusive rate of the per-step path; reported beside, never as `value`
+    kh = min(K, 500)
+    p1h, p2h = p1[W:W + kh].cpu().numpy(), p2[W:W + kh].cpu().numpy()
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(kh):
+        rc = fs_step(h, p1h[k].ctypes.data, p2h[k].ctypes.data, _abi.FS_ACT_HOST)
+        if rc:
+            check(rc, h)
+    torch.cuda.synchronize(dev)
+    host_rate = N * kh / (time.perf_counter() - t0)
     # dominant kernel of the reported mode, back-to-back launches
     if args.mode == "fused":
         kt, kmed = kernel_time(run_fused, W, max(5, args.kernel_samples // 10), chunk)
@@ -172,6 +202,9 @@ def main():
         kt, kmed = kernel_time(run_step, W, args.kernel_samples, 1)
         bytes_per_launch = N * (STATE_BYTES + STEP_IO_BYTES)
     achieved = bytes_per_launch / kt / 1e9
+    kname = "fsk::k_step_n<0, 0>" if args.mode == "fused" else "fsk::k_step<0, 0>"
+    ticks = chunk if args.mode == "fused" else 1
+    tr = pmc_traffic(kname, N, ticks)
     other = "step" if args.mode == "fused" else "fused"
     out = {
         "metric": METRIC,
@@ -190,10 +223,13 @@ def main():
                    "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
                    "ticks_per_launch": chunk if args.mode == "fused" else 1, "parallelism": "arena-shard x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": "fsk::k_step<0,0>", "avg_launch_us": kt * 1e6, "median_launch_us": kmed * 1e6,
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": tr[0] if tr else None,
+                     "traffic_source": tr[1] if tr else None,
+                     "kernel": kname, "avg_launch_us": kt * 1e6, "median_launch_us": kmed * 1e6,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
+        "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
+                                   "note": "fs_step with FS_ACT_HOST (PCIe-inclusive action hand-over)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)

@@ -21,7 +21,7 @@ HEADERS = ["fs_internal.h", "fs_tables.h"]
 #   of the action state machine into one store through a pointer phi, which blocks SROA and
 #   leaves the whole per-lane arena (272 B) in scratch memory -- 400+ scratch ops per tick.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
-          "-fno-fast-math", "-Wall", "-Wno-unused-function", "-mllvm", "-simplifycfg-sink-common=false"]
+          "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-bitwise-instead-of-logical", "-mllvm", "-simplifycfg-sink-common=false"]
 
 
 def _hipcc():

@@ -983,8 +983,11 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   }
 }
 
-template <int FM, int P2>
-__global__ __launch_bounds__(256) void k_step(StepParams p) {
+// One launch over all arenas, `TICKS` = 1 (k_step, the per-step VectorEnv path) or
+// p.n_steps (k_step_n*, the fused rollout: state stays in registers between ticks).
+// HASH draws the actions in-kernel from splitmix64 instead of reading action rows.
+template <int FM, int P2, bool FUSED, bool HASH>
+__device__ __forceinline__ void step_body(const StepParams& p) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   constexpr bool BOT = P2 == FS_P2_BOT;
   const bool active = l < 2 * p.n_envs;
@@ -997,8 +1000,8 @@ __global__ __launch_bounds__(256) void k_step(StepParams p) {
   const bool reads = k == 0 || P2 == FS_P2_EXTERNAL;
   auto fetch = [&](int t) -> uint32_t {
     if (!reads) return 0u;
-    return src ? src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a]
-               : hash_action(p.action_seed, a, p.t0 + (uint64_t)t, k);
+    if constexpr (HASH) return hash_action(p.action_seed, a, p.t0 + (uint64_t)t, k);
+    else return src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a];
   };
   // the arena state and the first action are in flight while the block stages the tables
   Lane L;
@@ -1006,13 +1009,32 @@ __global__ __launch_bounds__(256) void k_step(StepParams p) {
   uint32_t next = fetch(0);
   stage_tables();
   if (!active) return;
-  const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
-  for (int t = 0; t < p.n_steps; t++) {
-    const uint32_t act = next;
-    if (t + 1 < p.n_steps) next = fetch(t + 1);
-    env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a);
+  if constexpr (FUSED) {
+    const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
+    for (int t = 0; t < p.n_steps; t++) {
+      const uint32_t act = next;
+      if (t + 1 < p.n_steps) next = fetch(t + 1);
+      env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a);
+    }
+  } else {
+    env_step<FM, P2>(L, next & 7u, p, (uint32_t)a);
   }
   store_lane<BOT>(L, p.st, a);
+}
+
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step(StepParams p) {
+  step_body<FM, P2, false, false>(p);
+}
+
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step_n(StepParams p) {
+  step_body<FM, P2, true, false>(p);
+}
+
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step_n_hashed(StepParams p) {
+  step_body<FM, P2, true, true>(p);
 }
 
 // FootsiesEnv.reset (FE:482-515) / RESET (BC:143-146) / game start (BC:105-128)
@@ -1212,12 +1234,20 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
 // ---------------------------------------------------------------------------
 static inline dim3 grid_for(int n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
 
+template <int FM, int P2>
+static void launch_step_p2(const StepParams& p, hipStream_t s) {
+  const dim3 grid = grid_for(2 * p.n_envs), block(kBlock);
+  if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
+  else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
+}
+
 template <int FM>
 static hipError_t launch_step_fm(const StepParams& p, int p2_mode, hipStream_t s) {
   switch (p2_mode) {
-    case FS_P2_EXTERNAL: hipLaunchKernelGGL((k_step<FM, FS_P2_EXTERNAL>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
-    case FS_P2_BOT: hipLaunchKernelGGL((k_step<FM, FS_P2_BOT>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
-    default: hipLaunchKernelGGL((k_step<FM, FS_P2_NOOP>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
+    case FS_P2_EXTERNAL: launch_step_p2<FM, FS_P2_EXTERNAL>(p, s); break;
+    case FS_P2_BOT: launch_step_p2<FM, FS_P2_BOT>(p, s); break;
+    default: launch_step_p2<FM, FS_P2_NOOP>(p, s); break;
   }
   return hipGetLastError();
 }
