@@ -91,6 +91,7 @@ struct Fighter {
   int rec;        // FrameRec index of (action, frame)
   uint32_t info;  // FrameRec::info (box counts, hitbox attack bits)
   float px, ux0, ux1, hx0, hx1;
+  float pw, pymin, pymax;  // pushbox width, yMin, yMax of the record
 };
 
 struct Arena {
@@ -299,6 +300,7 @@ __device__ __forceinline__ bool ai_always_cancel(AInfo i) { return (i.y & 0xffu)
 __device__ __forceinline__ int ai_cancel_lo(AInfo i) { return (int)((i.y >> 16) & 0xffu); }
 __device__ __forceinline__ int ai_cancel_hi(AInfo i) { return (int)(i.y >> 24); }
 __device__ __forceinline__ uint32_t ai_cancel_mask(AInfo i) { return i.z; }
+__device__ __forceinline__ int ai_rec0(AInfo i) { return (int)i.w; }
 static_assert(sizeof(ActionInfo) == 16, "ActionInfo must be 16 bytes");
 
 // RequestAction (F:472-510), branch-free.  `ai` is the ActionInfo of f.act (kept
@@ -332,7 +334,8 @@ __device__ __forceinline__ void increment_action_frame(Fighter& f, AInfo ai) {
 
 // UpdateActionRequest (F:201-286).  Every request target is decided from the inputs
 // and the state before the first request, so the four ActionInfo reads are issued
-// together; the request chain itself is branch-free.
+// together; the request chain itself is branch-free.  On return `ai` is the
+// ActionInfo of f.act.
 __device__ __forceinline__ void update_action_request(Fighter& f, const InputEval& e, AInfo& ai) {
   if (f.won) {  // F:204-208 (hasWon is only set between KO and the next SetupBattleStart)
     request_action(f, ai, A_WIN, action_info(A_WIN), true);
@@ -354,8 +357,12 @@ __device__ __forceinline__ void update_action_request(Fighter& f, const InputEva
                  : e.fwd          ? A_FORWARD
                  : e.back         ? (f.prox ? A_GUARD_PROXIMITY : A_BACKWARD)
                                   : A_STAND;
-  const AInfo i1 = action_info(a1), i2 = action_info(a2), i3 = action_info(a3);
+  AInfo i0 = action_info(early ? a0 : 0), i1 = action_info(a1), i2 = action_info(a2), i3 = action_info(a3);
+  // materialise all four here: left alone, the compiler sinks a read into the branch it
+  // makes of a request's `take`, a second dependent LDS round trip
+  asm volatile("" : "+v"(i0), "+v"(i1), "+v"(i2), "+v"(i3));
   f.act = early ? a0 : f.act;
+  ai = early ? i0 : ai;
   f.frame = early ? 0 : f.frame;
   f.hits = early ? 0 : f.hits;
   f.buf = early ? NONE : f.buf;
@@ -378,7 +385,7 @@ __device__ __forceinline__ void update_movement(Fighter& f, float sign, float re
   f.x = (f.stun <= 0 && v != 0.0f) ? nx : f.x;
 }
 
-// the frame record of (act, frame) after the action request
+// the frame record of (act, frame)
 __device__ __forceinline__ int frame_record(const Fighter& f) {
   return sT.rec_index[f.act * kFrameStride + min(f.frame, kFrameStride - 1)];
 }
@@ -387,6 +394,9 @@ __device__ __forceinline__ int frame_record(const Fighter& f) {
 template <int FM>
 __device__ __forceinline__ void update_boxes(Fighter& f, float sign, const FrameRec& R) {
   f.info = R.info;
+  f.pw = R.push.y;
+  f.pymin = R.push.z;
+  f.pymax = R.push.w;
   f.px = xform<FM>(f.x, R.push.x, sign);
   f.ux0 = xform<FM>(f.x, R.hurt[0].x, sign);
   f.ux1 = xform<FM>(f.x, R.hurt[1].x, sign);
@@ -408,7 +418,7 @@ __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
 // UpdatePushCharacterVsBackground (BC:503-519) with BoxBase semantics
 template <int FM>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
-  const float w = sT.recs[f.rec].push.y;
+  const float w = f.pw;
   const float xmin = bb_xmin<FM>(f.px, w);
   if (xmin < -kStageHalf) {
     apply_position_change<FM>(f, fsub<FM>(-kStageHalf, xmin));
@@ -660,6 +670,7 @@ struct Lane {
   double cum;
   uint32_t rec;       // this player's recordingPnInput[index - 1]
   uint32_t act;       // this player's TrainingActor.GetInput()
+  AInfo ai;           // ActionInfo of f.act (reloaded at the end of every tick)
   Bot bot;            // P2 lane, FS_P2_BOT only
 };
 
@@ -722,11 +733,12 @@ __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int
 template <int FM>
 __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t k) {
   const float o_px = xpair(f.px), o_x = xpair(f.x);
-  const int o_rec = xpair(f.rec);
+  const float o_pw = xpair(f.pw), o_pymin = xpair(f.pymin), o_pymax = xpair(f.pymax);
   const float px1 = k == 0 ? f.px : o_px, px2 = k == 0 ? o_px : f.px;
   const float x1 = k == 0 ? f.x : o_x, x2 = k == 0 ? o_x : f.x;
   // record pushboxes are (x offset, width, yMin, yMax); position.y == 0
-  const float4 r1 = sT.recs[k == 0 ? f.rec : o_rec].push, r2 = sT.recs[k == 0 ? o_rec : f.rec].push;
+  const float4 mine = make_float4(0.0f, f.pw, f.pymin, f.pymax), theirs = make_float4(0.0f, o_pw, o_pymin, o_pymax);
+  const float4 r1 = k == 0 ? mine : theirs, r2 = k == 0 ? theirs : mine;
   const float xmax1 = fadd<FM>(r1.y, px1), xmax2 = fadd<FM>(r2.y, px2);
   const bool overlap = (xmax2 > px1) & (px2 < xmax1) & (r2.w > r1.z) & (r2.z < r1.w);
   if (!overlap || x1 == x2) return;  // a tie pushes nothing (BC:490-499)
@@ -900,8 +912,15 @@ __device__ __forceinline__ uint32_t hash_action(uint64_t seed, uint64_t env, uin
 // one env-step: FootsiesEnv.step (FE:518-570) over the synced game's Fight tick
 // (BC:201-220, 347-364) and, for a terminal arena, the auto-reset burst
 // ---------------------------------------------------------------------------
+// `next` is the next tick's action, loaded by the caller before this tick: it is made
+// resident before this tick's first store.  Loads and stores share one in-order
+// counter (vmcnt) on gfx9, so a wait for `next` placed after the stores (where the
+// compiler would put it, at the loop latch) would also wait for every store of the
+// tick to be acknowledged by memory.
+__device__ __forceinline__ void settle(uint32_t& next) { asm volatile("" : "+v"(next)); }
+
 template <int FM, int P2>
-__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r) {
+__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   const DevOutputs& o = p.out;
   const uint32_t k = L.k;
@@ -910,6 +929,8 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.pending = false;
     L.has_term = false;
     L.cum = 0.0;
+    L.ai = action_info(L.f.act);
+    settle(next);
     write_main(L, o, r);
     if (k == 0) {
       o.reward[r] = 0.0;
@@ -929,10 +950,13 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   }
   const float sign = k == 0 ? 1.0f : -1.0f;
   const InputEval e = update_input(L.f, L.act, (int)k);
-  AInfo ai = action_info(L.f.act);
+  AInfo ai = L.ai;  // ActionInfo of f.act, carried from the previous tick
   increment_action_frame(L.f, ai);
+  // the record if the action continues, read alongside the request's ActionInfo reads;
+  // a request that changes (or restarts) the action sets frame 0, whose record is ai.rec0
+  const int rec_cont = frame_record(L.f);
   update_action_request(L.f, e, ai);
-  L.f.rec = frame_record(L.f);
+  L.f.rec = L.f.frame == 0 ? ai_rec0(ai) : rec_cont;
   const FrameRec& R = sT.recs[L.f.rec];
   update_movement<FM>(L.f, sign, R.vel);
   update_boxes<FM>(L.f, sign, R);
@@ -955,6 +979,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   } else {
     reward = over ? (v2 == 0 ? 1.0 : -1.0) : 0.0;
   }
+  settle(next);
   if (over) {
     L.f.hist = 0;  // ChangeRoundState(KO): ClearInput (BC:296-299)
     L.f.hold = 0;
@@ -975,6 +1000,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     }
     L.has_term = false;
   }
+  L.ai = action_info(L.f.act);  // hits and resets set actions too; its latency hides behind the stores
   write_main(L, o, r);
   if (k == 0) {
     o.reward[r] = reward;
@@ -1009,15 +1035,17 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   uint32_t next = fetch(0);
   stage_tables();
   if (!active) return;
+  L.ai = action_info(L.f.act);
   if constexpr (FUSED) {
     const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
     for (int t = 0; t < p.n_steps; t++) {
       const uint32_t act = next;
-      if (t + 1 < p.n_steps) next = fetch(t + 1);
-      env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a);
+      next = fetch(min(t + 1, p.n_steps - 1));  // the last tick re-reads its own row
+      env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
     }
   } else {
-    env_step<FM, P2>(L, next & 7u, p, (uint32_t)a);
+    uint32_t none = 0;
+    env_step<FM, P2>(L, next & 7u, p, (uint32_t)a, none);
   }
   store_lane<BOT>(L, p.st, a);
 }
