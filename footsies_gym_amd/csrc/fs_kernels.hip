@@ -13,8 +13,9 @@
 // the velocity and the hitbox attack bits -- the window scans of
 // ActionData.cs:87-168 resolved offline (tools/gen_tables.py).  A tick needs
 // four dependent LDS round trips: action info, requested actions' infos, record
-// index, record.  The 180-deep input histories (Fighter.cs:98-101) are a 16-frame
-// Left/Right shift register plus a saturating attack-hold counter: the reference
+// index, record.  The 180-deep input histories (Fighter.cs:98-101) are two 16-frame
+// shift registers (backward / forward relative to the fighter's facing) plus a
+// saturating attack-hold counter: the reference
 // only reads input[0..16] for dashes (Fighter.cs:585-635, dashAllowFrame 9) and
 // "attack held on input[1..59]" for the charge special (Fighter.cs:569-583).
 //
@@ -83,7 +84,7 @@ __device__ __forceinline__ void stage_tables() {
 
 struct Fighter {
   float x;
-  uint32_t hist;  // raw Left/Right bits of input[0..15]
+  uint32_t hist;  // input[0..15]: bit j = backward on input[j], bit 16 + j = forward (see split_hist)
   int act, frame, stun, vital, guard, hits, buf, rsv, hold;
   bool in_back, prox, won;
   // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
@@ -139,7 +140,7 @@ __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
   unpack_fighter(A.f1, pk.z, pk.w);
   A.f0.x = pos.x;
   A.f1.x = pos.y;
-  A.f0.hist = hist.x;
+  A.f0.hist = hist.x;  // split form (get/set convert)
   A.f1.hist = hist.y;
   A.frame_count = aw.x;
   uint32_t h = (uint32_t)aw.y;
@@ -237,9 +238,6 @@ __device__ __forceinline__ uint32_t rel_bits(uint32_t in, int k) {
   in &= 3;
   return k == 0 ? in : (((in & 1) << 1) | (in >> 1));
 }
-__device__ __forceinline__ uint32_t rel_hist(uint32_t h, int k) {
-  return k == 0 ? h : (((h & 0x55555555u) << 1) | ((h >> 1) & 0x55555555u));
-}
 __device__ __forceinline__ uint32_t compact_even(uint32_t x) {
   x &= 0x55555555u;
   x = (x | (x >> 1)) & 0x33333333u;
@@ -248,23 +246,42 @@ __device__ __forceinline__ uint32_t compact_even(uint32_t x) {
   x = (x | (x >> 8)) & 0x0000FFFFu;
   return x;
 }
+__device__ __forceinline__ uint32_t spread_even(uint32_t x) {
+  x &= 0x0000FFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+// The state API's history is raw Left/Right bit pairs per frame (input[j] at bits
+// 2j, 2j+1); the kernels keep the facing-relative split form, so a tick shifts two
+// registers at once and the dash parsers read them directly.
+__device__ __forceinline__ uint32_t split_hist(uint32_t raw, int k) {
+  const uint32_t rel = k == 0 ? raw : (((raw & 0x55555555u) << 1) | ((raw >> 1) & 0x55555555u));
+  return compact_even(rel) | (compact_even(rel >> 1) << 16);
+}
+__device__ __forceinline__ uint32_t raw_hist(uint32_t h, int k) {
+  const uint32_t b = spread_even(h), f = spread_even(h >> 16);
+  return k == 0 ? (b | (f << 1)) : (f | (b << 1));
+}
 
 // UpdateInput + the reads UpdateActionRequest makes of the new history.
 __device__ __forceinline__ InputEval update_input(Fighter& f, uint32_t in, int k) {
   const uint32_t old_hist = f.hist;
   const int old_hold = f.hold;
-  const uint32_t in1 = (old_hist & 3) | (old_hold > 0 ? IN_ATTACK : 0);  // input[1] after the shift
-  f.hist = (old_hist << 2) | (in & 3);
+  const uint32_t r0 = rel_bits(in, k);
+  const uint32_t r1 = (old_hist & 1) | ((old_hist >> 15) & 2);  // input[1] after the shift, relative
+  f.hist = ((old_hist << 1) & 0xFFFEFFFEu) | (r0 & 1) | ((r0 & 2) << 15);
   f.hold = (in & IN_ATTACK) ? min(old_hold + 1, 63) : 0;
+  const bool in1_atk = old_hold > 0;
   InputEval e;
-  const uint32_t r0 = rel_bits(in, k), r1 = rel_bits(in1, k);
   e.fwd = r0 & 2;
   e.back = r0 & 1;
-  e.atk_down = (in & IN_ATTACK) && !(in1 & IN_ATTACK);                   // inputDown[0] & Attack
+  e.atk_down = (in & IN_ATTACK) && !in1_atk;                            // inputDown[0] & Attack
   e.special = !(in & IN_ATTACK) && old_hold >= kSpecialHoldFrame - 1;  // inputUp[0] & Attack, input[1..59] held
   // dash parsers over input[1..16] (bit j-1 of each mask = input[j])
-  const uint32_t rh = rel_hist(old_hist, k);
-  const uint32_t B = compact_even(rh), F = compact_even(rh >> 1), E = B | F;
+  const uint32_t B = old_hist & 0xFFFFu, F = old_hist >> 16, E = B | F;
   const uint32_t win = (1u << (kDashAllowFrame - 1)) - 1u;
   const uint32_t e8 = E & win;
   e.fdash = false;
@@ -858,7 +875,8 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
     L.rec = L.act;
     L.rec_count++;
   }
-  L.f.hist = L.act & 3;
+  const uint32_t r = rel_bits(L.act, (int)L.k);
+  L.f.hist = (r & 1) | ((r & 2) << 15);
   L.f.hold = (L.act & IN_ATTACK) ? 1 : 0;
   const bool stunned = L.f.stun > 0;
   L.f.stun -= stunned ? 1 : 0;
@@ -1148,7 +1166,7 @@ __global__ __launch_bounds__(256) void k_get_state(DevState st, fs_arena_state* 
       g.guard = f.guard;
       g.buffer_action_id = f.buf == NONE ? -1 : kActionId[f.buf];
       g.reserve_action_id = f.rsv == NONE ? -1 : kActionId[f.rsv];
-      g.input_dir_history = f.hist;
+      g.input_dir_history = raw_hist(f.hist, k);
       g.attack_hold = f.hold;
       g.is_input_backward = f.in_back;
       g.is_reserve_proximity_guard = f.prox;
@@ -1230,7 +1248,7 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
     f.guard = g.guard;
     f.buf = g.buffer_action_id < 0 ? NONE : action_index_of(g.buffer_action_id);
     f.rsv = g.reserve_action_id < 0 ? NONE : action_index_of(g.reserve_action_id);
-    f.hist = g.input_dir_history;
+    f.hist = split_hist(g.input_dir_history, k);
     f.hold = g.attack_hold;
     f.in_back = g.is_input_backward;
     f.prox = g.is_reserve_proximity_guard;
