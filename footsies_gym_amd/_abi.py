@@ -32,6 +32,7 @@ FS_STREAM_OWN = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)
 FS_RESET_HARD = 0
 FS_RESET_IF_NEEDED = 1
 FS_RESET_SEED_ONLY = 2
+FS_MAX_FRAME_DELAY = 4096
 
 # InputDefine (Assets/Script/InputData.cs:8-14)
 IN_LEFT, IN_RIGHT, IN_ATTACK = 1, 2, 4

@@ -52,6 +52,7 @@ struct fs_context {
   uint8_t* d_mask = nullptr;     // [N]
   uint8_t* h_mask = nullptr;     // pinned [N]
   hipEvent_t staging_free = nullptr;
+  uint4* delay_ring = nullptr;   // frame_delay > 0: [d][N] x 32-B observation records (fs_delay.hip)
   std::vector<void*> allocations;
   uint64_t steps = 0;
   std::string err;
@@ -114,6 +115,23 @@ void outputs_from_own(fs_context* h) {
                            b.f_move_frame, b.f_position, b.f_frame, b.f_action, b.f_hitstun};
 }
 
+// FootsiesEnv's delayed-frame queue over rows the last kernel wrote (no-op for frame_delay 0)
+int apply_delay(fs_context* h, const fsk::DevOutputs& out, int n_steps, int stride, bool refill_only) {
+  if (h->cfg.frame_delay <= 0) return FS_OK;
+  fsk::DelayParams dp{};
+  dp.out = out;
+  dp.ring = h->delay_ring;
+  dp.n_envs = h->n;
+  dp.delay = h->cfg.frame_delay;
+  dp.n_steps = n_steps;
+  dp.out_stride_steps = stride;
+  dp.step0 = h->steps;
+  dp.refill_only = refill_only ? 1 : 0;
+  dp.same_step = h->cfg.autoreset_mode == FS_AUTORESET_SAME_STEP;
+  HIP_TRY(h, fsk::launch_delay(dp, h->stream));
+  return FS_OK;
+}
+
 // wait until the pinned staging buffers may be overwritten
 int staging_wait(fs_context* h) {
   HIP_TRY(h, hipEventSynchronize(h->staging_free));
@@ -135,8 +153,9 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
     return set_err(nullptr, FS_E_INVALID, "invalid float_mode %d", cfg->float_mode);
   if (cfg->autoreset_mode != FS_AUTORESET_SAME_STEP && cfg->autoreset_mode != FS_AUTORESET_NEXT_STEP)
     return set_err(nullptr, FS_E_INVALID, "invalid autoreset_mode %d", cfg->autoreset_mode);
-  if (cfg->frame_delay != 0)
-    return set_err(nullptr, FS_E_UNSUPPORTED, "frame_delay=%d is not supported (only 0)", cfg->frame_delay);
+  if (cfg->frame_delay < 0 || cfg->frame_delay > FS_MAX_FRAME_DELAY)
+    return set_err(nullptr, FS_E_INVALID, "frame_delay must be in [0, %d] (got %d)", FS_MAX_FRAME_DELAY,
+                   cfg->frame_delay);
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev <= 0)
@@ -183,6 +202,7 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   // staging
   if ((rc = dalloc(h, &h->d_act, 2 * N)) || (rc = dalloc(h, &h->d_seeds, N)) || (rc = dalloc(h, &h->d_mask, N)))
     return fail(rc);
+  if (cfg->frame_delay > 0 && (rc = dalloc(h, &h->delay_ring, 2 * (size_t)cfg->frame_delay * N))) return fail(rc);
   if (hipHostMalloc((void**)&h->h_act, 2 * N, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&h->h_seeds, N * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&h->h_mask, N, hipHostMallocDefault) != hipSuccess)
@@ -206,6 +226,7 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   rp.base_seed = cfg->base_seed;
   hipError_t le = fsk::launch_reset(rp, cfg->float_mode, cfg->p2_mode, h->stream);
   if (le != hipSuccess) return fail(set_err(h, FS_E_DEVICE, "reset kernel launch: %s", hipGetErrorString(le)));
+  if ((rc = apply_delay(h, h->out, 1, 0, true))) return fail(rc);  // the first reset's queue (FE:502-504)
   le = hipStreamSynchronize(h->stream);
   if (le != hipSuccess) return fail(set_err(h, FS_E_DEVICE, "reset kernel: %s", hipGetErrorString(le)));
   *out = h;
@@ -239,6 +260,7 @@ FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int
   }
   HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
   HIP_TRY(h, fsk::launch_reset(rp, h->cfg.float_mode, h->cfg.p2_mode, h->stream));
+  if (flags != FS_RESET_SEED_ONLY && (rc = apply_delay(h, h->out, 1, 0, true))) return rc;
   return FS_OK;
 }
 
@@ -286,8 +308,18 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
          !traj->final_frame || !traj->final_action || !traj->final_hitstun))
       return set_err(h, FS_E_INVALID, "fs_step_n: final_* trajectory buffers required in same-step autoreset");
     sp.out_stride_steps = 1;
+  } else if (n > 1 && h->cfg.frame_delay > 0) {
+    // the delayed queue needs every step's row, which a fused launch without a
+    // trajectory overwrites: step one tick per launch instead
+    for (int j = 0; j < n; j++) {
+      const uint8_t* q1 = sp.p1 ? sp.p1 + (size_t)j * N : nullptr;
+      const uint8_t* q2 = sp.p2 ? sp.p2 + (size_t)j * N : nullptr;
+      if ((rc = step_common(h, 1, q1, q2, FS_ACT_DEVICE, seed, nullptr))) return rc;
+    }
+    return FS_OK;
   }
   HIP_TRY(h, fsk::launch_step(sp, h->cfg.float_mode, h->cfg.p2_mode, h->stream));
+  if ((rc = apply_delay(h, sp.out, n, sp.out_stride_steps, false))) return rc;
   h->steps += (uint64_t)n;
   return FS_OK;
 }

@@ -12,7 +12,7 @@ namespace fsk {
 // vectors so one wave64 load/store moves 512 B / 1 KiB contiguous).
 struct DevState {
   float2* pos;     // x of P1, P2 (Fighter.position.x)
-  uint2* hist;     // Left/Right bits of input[0..15] per fighter, input[0] in bits 0-1
+  uint2* hist;     // per fighter: bit j = backward on input[j], bit 16 + j = forward (facing-relative)
   uint4* fpk;      // packed fighter words: (P1 lo, P1 hi, P2 lo, P2 hi), layout in fs_kernels.hip
   int2* aw;        // (frameCount, arena header word)
   double* cum;     // FootsiesEnv._cummulative_episode_reward
@@ -65,7 +65,23 @@ struct ResetParams {
   uint64_t base_seed;
 };
 
-// launchers (fs_kernels.hip); return hipError_t of the launch
+// FootsiesEnv's delayed-frame queue (FE:126-131, 493-504, 532-535) for frame_delay = d > 0:
+// per arena a ring of d packed observation records, slot = global step index mod d
+// (all arenas step together).  Applied after a step kernel to the rows it wrote, or
+// after a reset to refill the rings of fresh arenas (output frame == -1).
+struct DelayParams {
+  DevOutputs out;
+  uint4* ring;          // [d][N] records of 2 x uint4 (layout in fs_delay.hip)
+  int n_envs;
+  int delay;            // d
+  int n_steps;          // rows to process (1 for fs_step / fs_reset)
+  int out_stride_steps;
+  uint64_t step0;       // global step index of the first row
+  int refill_only;      // 1: after fs_reset / fs_create (no queue shift)
+  int same_step;        // FS_AUTORESET_SAME_STEP: a terminal row's final_* take the delayed record
+};
+
+// launchers (fs_kernels.hip, fs_delay.hip); return hipError_t of the launch
 hipError_t launch_step(const StepParams& p, int float_mode, int p2_mode, hipStream_t s);
 hipError_t launch_reset(const ResetParams& p, int float_mode, int p2_mode, hipStream_t s);
 hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1, uint8_t* p2,
@@ -73,5 +89,6 @@ hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t 
 hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_state* env_dst, int n, int p2_mode,
                             hipStream_t s);
 hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, int p2_mode, hipStream_t s);
+hipError_t launch_delay(const DelayParams& p, hipStream_t s);
 
 }  // namespace fsk

@@ -15,6 +15,7 @@ Differences from the reference, by design:
 """
 import numpy as np
 
+from . import _abi
 from . import spaces as sp
 from .simulator import FootsiesSim, decode_actions, encode_actions
 
@@ -67,7 +68,8 @@ class FootsiesVectorEnv:
     """N FOOTSIES arenas as one vector environment.
 
     Parameters follow FootsiesEnv.__init__ (FE:34-53) where they still have a
-    meaning: ``frame_delay`` (only 0), ``dense_reward``, ``opponent``:
+    meaning: ``frame_delay`` (observations and info ``frame_delay`` steps old, FE:126-131,
+    532-535; reward and termination current), ``dense_reward``, ``opponent``:
       * ``None`` -> the in-game scripted bot as P2 (FE:236-237, ``--p2-bot``);
       * a callable ``opponent(obs, info) -> actions`` -> P2 driven by that policy,
         called every step with the most recent batched obs/info (FE:525-527);
@@ -84,8 +86,8 @@ class FootsiesVectorEnv:
             raise ValueError("vs_player needs a human at the game window; not available in the simulator")
         if by_example:
             raise ValueError("by_example (the bot playing P1) is not supported")
-        if frame_delay != 0:
-            raise ValueError("frame_delay > 0 is not supported yet (FE:126-131)")
+        if not 0 <= int(frame_delay) <= _abi.FS_MAX_FRAME_DELAY:
+            raise ValueError("frame_delay must be in [0, %d]" % _abi.FS_MAX_FRAME_DELAY)
         if output not in ("numpy", "torch"):
             raise ValueError("output must be 'numpy' or 'torch'")
         self.num_envs = int(num_envs)

@@ -35,7 +35,7 @@ extern "C" {
 #define FS_OK 0
 #define FS_E_INVALID (-1)      /* bad argument (FE:100-108 raises ValueError for bad ctor args) */
 #define FS_E_DEVICE (-2)       /* HIP runtime failure / no device */
-#define FS_E_UNSUPPORTED (-3)  /* configuration not implemented (e.g. frame_delay > 0) */
+#define FS_E_UNSUPPORTED (-3)  /* configuration not implemented */
 #define FS_E_OOM (-4)
 
 /* P2 controller (GameManager.cs:183-190: --p2-bot / remote actor; FE:234-247) */
@@ -64,12 +64,17 @@ extern "C" {
 #define FS_RESET_SEED_ONLY 2    /* SEED command alone (BC:170-173): Random.InitState on the masked
                                    arenas, nothing else changes and no outputs are written */
 
+#define FS_MAX_FRAME_DELAY 4096
+
 typedef struct fs_config {
   int32_t num_envs;        /* arenas on this handle (>0) */
   int32_t device_id;       /* HIP device ordinal */
   int32_t p2_mode;         /* FS_P2_* */
   int32_t dense_reward;    /* 1: FE._get_dense_reward (FE:388-405, default FE:50); 0: sparse (FE:382-386) */
-  int32_t frame_delay;     /* FE:36,129-131; only 0 is supported */
+  int32_t frame_delay;     /* FE:36, 126-131, 493-504, 532-535: observation/info outputs are those of
+                              the state frame_delay steps back (d copies of state(-1) after a reset);
+                              reward, terminated and fs_get_env_state are the newest state's.
+                              0 .. FS_MAX_FRAME_DELAY */
   int32_t float_mode;      /* FS_FLOAT_* */
   int32_t autoreset_mode;  /* FS_AUTORESET_* */
   int32_t reserved0;
@@ -168,7 +173,7 @@ int fs_abi_version(void);
 /* Create N arenas on a device and run the game-start sequence (BattleCore.Start
  * + first Stop->Intro->Fight ticks, BC:105-128, 176-200, 262-291) so they sit at
  * state(-1).  Replaces FootsiesEnv.__init__ + _instantiate_game + _connect_to_game
- * (FE:34-290).  Returns FS_E_UNSUPPORTED for frame_delay != 0. */
+ * (FE:34-290).  Returns FS_E_INVALID for an out-of-range field. */
 int fs_create(const fs_config* cfg, fs_handle* out);
 
 /* Reset arenas (FootsiesEnv.reset, FE:482-515).  seeds: optional host array [N]
@@ -190,7 +195,9 @@ int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags
  * a = splitmix64(action_seed ^ env*0x9E3779B97F4A7C15 ^ (t << 1 | player)) & 7
  * with t = fs_steps_taken(h) + k.  traj: device arrays laid out [n][N] (pairs
  * [n][N][2]) receiving every tick's outputs; traj == NULL writes each tick
- * into the handle's regular outputs (the last tick remains visible). */
+ * into the handle's regular outputs (the last tick remains visible; with
+ * frame_delay > 0 the n ticks are then launched one by one, since the delayed
+ * queue consumes every tick's row). */
 int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act,
               uint64_t action_seed, const fs_outputs* traj);
 

@@ -174,6 +174,8 @@ typedef struct {
   double cum_reward;         /* FE._cummulative_episode_reward */
   int has_terminated;        /* FE.has_terminated */
   int reset_pending;         /* FS_AUTORESET_NEXT_STEP */
+  fs_env_state* dq;          /* FE.delayed_frame_queue (FE:129-131), capacity frame_delay + 1 */
+  int dq_head, dq_count;
   /* emission bookkeeping of one driver call */
   int emitted;
   int emitted_battle_over;
@@ -1028,6 +1030,24 @@ static void write_final_obs(or_ctx* C, int i, const obs_t* o) {
   C->f_frame[i] = o->frame;
 }
 
+/* FE.delayed_frame_queue, a deque(maxlen = frame_delay + 1) of raw states (FE:129-131) */
+static void dq_clear(arena_t* A) { A->dq_head = A->dq_count = 0; }
+static void dq_append(or_ctx* C, arena_t* A, const fs_env_state* s) {
+  int cap = C->cfg.frame_delay + 1;
+  if (A->dq_count == cap) { /* a full deque drops its oldest entry */
+    A->dq_head = (A->dq_head + 1) % cap;
+    A->dq_count--;
+  }
+  A->dq[(A->dq_head + A->dq_count) % cap] = *s;
+  A->dq_count++;
+}
+static fs_env_state dq_popleft(or_ctx* C, arena_t* A) {
+  fs_env_state s = A->dq[A->dq_head];
+  A->dq_head = (A->dq_head + 1) % (C->cfg.frame_delay + 1);
+  A->dq_count--;
+  return s;
+}
+
 /* FootsiesEnv.reset body after the (optional) RESET: read states until frame -1 */
 static void fe_reset_arena(or_ctx* C, int i, const uint64_t* seeds, int hard) {
   arena_t* A = &C->a[i];
@@ -1039,6 +1059,8 @@ static void fe_reset_arena(or_ctx* C, int i, const uint64_t* seeds, int hard) {
   A->cum_reward = 0.0;
   A->cur_state = s;
   A->has_terminated = 0;
+  dq_clear(A); /* FE:493, 502-504: frame_delay copies of the first state */
+  while (A->dq_count < C->cfg.frame_delay) dq_append(C, A, &s);
   obs_t o = extract_obs_info(&s);
   write_obs(C, i, &o);
   C->reward[i] = 0.0;
@@ -1058,7 +1080,8 @@ static void fe_step_arena(or_ctx* C, int i, int p1, int p2) {
   fs_env_state prev = A->cur_state;
   fs_env_state st = run_until_emission(C, A, 0);
   A->cur_state = st;
-  fs_env_state obs_state = st;
+  dq_append(C, A, &st); /* FE:533-535: the newest state in, the oldest out */
+  fs_env_state obs_state = dq_popleft(C, A);
   obs_state.p1Move = dead_win_to_stand(obs_state.p1Move);
   obs_state.p2Move = dead_win_to_stand(obs_state.p2Move);
   obs_t o = extract_obs_info(&obs_state);
@@ -1106,7 +1129,7 @@ static void new_fighter(fighter_t* f) { /* `new Fighter()` (BC:93-94) field defa
 
 OR_EXPORT int or_create(const fs_config* cfg, or_handle* out) {
   if (!cfg || !out || cfg->num_envs <= 0) return FS_E_INVALID;
-  if (cfg->frame_delay != 0) return FS_E_UNSUPPORTED;
+  if (cfg->frame_delay < 0) return FS_E_INVALID;
   if (cfg->p2_mode < 0 || cfg->p2_mode > 2) return FS_E_INVALID;
   or_ctx* C = (or_ctx*)xcalloc(1, sizeof(or_ctx));
   C->cfg = *cfg;
@@ -1140,6 +1163,8 @@ OR_EXPORT int or_create(const fs_config* cfg, or_handle* out) {
     /* game start: Stop -> Intro -> Fight, state(-1) emitted */
     A->cur_state = run_until_emission(C, A, 0);
     A->has_terminated = 1; /* FE.__init__ (FE:191): the first reset() sends no RESET */
+    A->dq = (fs_env_state*)xcalloc((size_t)cfg->frame_delay + 1, sizeof(fs_env_state));
+    while (A->dq_count < cfg->frame_delay) dq_append(C, A, &A->cur_state);
     obs_t o = extract_obs_info(&A->cur_state);
     write_obs(C, i, &o);
   }
@@ -1292,6 +1317,7 @@ OR_EXPORT int or_get_threads(void) {
 
 OR_EXPORT void or_destroy(or_handle C) {
   if (!C) return;
+  for (int i = 0; i < C->n; i++) free(C->a[i].dq);
   free(C->a);
   free(C->guard); free(C->move); free(C->action); free(C->hitstun); free(C->terminated); free(C->truncated);
   free(C->move_frame); free(C->position); free(C->reward); free(C->frame);

@@ -4,8 +4,10 @@
 What is pinned: the FootsiesEnv post-processing layer (footsies.py:336-405,
 482-570): obs extraction, DEAD/WIN -> STAND substitution, move_frame
 simplification, move-id -> index mapping, info, dense/sparse reward with its
-float64 accumulation, termination, and the reset handshake (no RESET after a
-terminated episode).  The reference FootsiesEnv class is imported from
+float64 accumulation, termination, the reset handshake (no RESET after a
+terminated episode) and the delayed-frame queue (frame_delay, FE:126-131, 493-504,
+532-535; the game-side states do not depend on it, so the oracle feeding them runs
+with frame_delay 0 and the reference FE applies its own queue).  The reference FootsiesEnv class is imported from
 /root/reference with a throwaway `gymnasium` stub (tests/golden/_gym_stub) and
 driven exactly as its socket would drive it: `_receive_and_update_state` is fed
 Unity-style EnvironmentState JSON (JsonUtility field order, floats in shortest
@@ -88,11 +90,11 @@ def obs_row(obs, info):
     }
 
 
-def generate(name, p2_mode, dense, n, steps, seed, sticky):
+def generate(name, p2_mode, dense, n, steps, seed, sticky, frame_delay=0):
     ora = binding.Oracle(n, p2_mode=p2_mode, dense_reward=dense, autoreset_mode=_abi.FS_AUTORESET_NEXT_STEP,
                          base_seed=seed)
     rng = np.random.default_rng(seed + 1000)
-    envs = [FedEnv(dense_reward=dense) for _ in range(n)]
+    envs = [FedEnv(dense_reward=dense, frame_delay=frame_delay) for _ in range(n)]
     st = ora.env_state()
     for i, e in enumerate(envs):
         e.feed.append(state_json(st[i]))
@@ -138,7 +140,7 @@ def generate(name, p2_mode, dense, n, steps, seed, sticky):
 
     out = {"%s/p1" % name: p1s, "%s/p2" % name: p2s, "%s/reward" % name: rew, "%s/terminated" % name: term,
            "%s/is_reset" % name: is_reset,
-           "%s/config" % name: np.array([p2_mode, int(dense), n, steps, seed], dtype=np.int64)}
+           "%s/config" % name: np.array([p2_mode, int(dense), n, steps, seed, frame_delay], dtype=np.int64)}
     for key in first[0]:
         out["%s/first/%s" % (name, key)] = np.array([r[key] for r in first])
         out["%s/%s" % (name, key)] = stack(key, rows)
@@ -151,6 +153,9 @@ def main():
     data.update(generate("bot_dense", _abi.FS_P2_BOT, True, 16, 2000, 0, 0.5))
     data.update(generate("ext_dense", _abi.FS_P2_EXTERNAL, True, 16, 1500, 1, 0.3))
     data.update(generate("bot_sparse", _abi.FS_P2_BOT, False, 16, 1500, 2, 0.8))
+    data.update(generate("ext_delay3", _abi.FS_P2_EXTERNAL, True, 16, 1500, 3, 0.3, frame_delay=3))
+    data.update(generate("bot_delay1", _abi.FS_P2_BOT, False, 16, 1200, 4, 0.6, frame_delay=1))
+    data.update(generate("ext_delay16", _abi.FS_P2_EXTERNAL, True, 8, 800, 5, 0.5, frame_delay=16))
     np.savez_compressed(os.path.join(HERE, "fe_golden.npz"), **data)
     moves = {
         "id_to_index": {str(k): v for k, v in ref_moves.FOOTSIES_MOVE_ID_TO_INDEX.items()},

@@ -6,9 +6,11 @@ AR = {_abi.FS_AUTORESET_SAME_STEP: "same_step", _abi.FS_AUTORESET_NEXT_STEP: "ne
 
 
 class SimBackend:
-    def __init__(self, n, p2_mode=_abi.FS_P2_EXTERNAL, dense=True, autoreset=_abi.FS_AUTORESET_SAME_STEP, seed=0):
+    def __init__(self, n, p2_mode=_abi.FS_P2_EXTERNAL, dense=True, autoreset=_abi.FS_AUTORESET_SAME_STEP, seed=0,
+                 frame_delay=0):
         from footsies_gym_amd.simulator import FootsiesSim
-        self.sim = FootsiesSim(n, p2_mode=P2[p2_mode], dense_reward=dense, autoreset_mode=AR[autoreset], seed=seed)
+        self.sim = FootsiesSim(n, p2_mode=P2[p2_mode], dense_reward=dense, autoreset_mode=AR[autoreset], seed=seed,
+                               frame_delay=frame_delay)
 
     def reset(self):
         self.sim.reset()
@@ -22,5 +24,5 @@ class SimBackend:
         return self.sim.env_state()
 
 
-def make(n, p2_mode, dense, autoreset, seed):
-    return SimBackend(n, p2_mode, dense, autoreset, seed)
+def make(n, p2_mode, dense, autoreset, seed, frame_delay=0):
+    return SimBackend(n, p2_mode, dense, autoreset, seed, frame_delay)

@@ -84,7 +84,8 @@ def test_invalid_configs_rejected(lib):
     lib.fs_create.argtypes = [C.POINTER(_abi.fs_config), C.POINTER(C.c_void_p)]
     h = C.c_void_p()
     for kw, code in [({"num_envs": 0}, _abi.FS_E_INVALID), ({"num_envs": 4, "p2_mode": 9}, _abi.FS_E_INVALID),
-                     ({"num_envs": 4, "frame_delay": 2}, _abi.FS_E_UNSUPPORTED),
+                     ({"num_envs": 4, "frame_delay": -1}, _abi.FS_E_INVALID),
+                     ({"num_envs": 4, "frame_delay": _abi.FS_MAX_FRAME_DELAY + 1}, _abi.FS_E_INVALID),
                      ({"num_envs": 4, "float_mode": 7}, _abi.FS_E_INVALID)]:
         assert lib.fs_create(C.byref(_abi.fs_config(**kw)), C.byref(h)) == code, kw
 

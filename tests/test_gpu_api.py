@@ -48,6 +48,41 @@ def test_step_n_trajectory_matches_single_steps(oracle_lib):
     compare_states(ora.state(), b.get_state())
 
 
+@pytest.mark.parametrize("autoreset", ["same_step", "next_step"])
+def test_frame_delay_paths_match_oracle(oracle_lib, autoreset):
+    """frame_delay > 0 (FE:126-131, 532-535) through fs_step, fs_step_n with a trajectory
+    and fs_step_n without one (launched tick by tick) == the oracle's FE deque."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    N, T, D = 777, 260, 5
+    ar = {"same_step": _abi.FS_AUTORESET_SAME_STEP, "next_step": _abi.FS_AUTORESET_NEXT_STEP}[autoreset]
+    kw = dict(p2_mode="external", seed=11, frame_delay=D, autoreset_mode=autoreset)
+    a, b, c = FootsiesSim(N, **kw), FootsiesSim(N, **kw), FootsiesSim(N, **kw)
+    p1, p2 = a.hash_actions(T, seed=0xD1A)
+    traj = a.alloc_trajectory(T)
+    a.step_n(T, p1, p2, trajectory=traj)
+    c.step_n(T, p1, p2)
+    torch.cuda.synchronize()
+    tr = {k: v.cpu().numpy() for k, v in traj.items()}
+    ora = oracle_lib.Oracle(N, p2_mode=_abi.FS_P2_EXTERNAL, base_seed=11, frame_delay=D, autoreset_mode=ar)
+    h1, h2 = p1.cpu().numpy(), p2.cpu().numpy()
+    terminals = 0
+    for t in range(T):
+        b.step(p1[t], p2[t])
+        exp = ora.step(h1[t], h2[t])
+        terminals += int(exp["terminated"].sum())
+        compare_outputs(exp, b.outputs_numpy(), step=t)
+        compare_outputs(exp, {k: v[t] for k, v in tr.items()}, step=t)
+    compare_outputs(exp, c.outputs_numpy(), step=T - 1)
+    assert terminals > 0
+    # an explicit reset refills the queue: the next D observations repeat state(-1)
+    b.reset(hard=True)
+    ora.reset(flags=_abi.FS_RESET_HARD)
+    for t in range(D + 3):
+        b.step(h1[t], h2[t])
+        compare_outputs(ora.step(h1[t], h2[t]), b.outputs_numpy(), step=T + t)
+
+
 def test_hashed_actions_match_host_stream(oracle_lib):
     """fs_hash_actions / in-kernel hashing == the splitmix64 stream of SURVEY.md §8(d)."""
     from footsies_gym_amd.simulator import FootsiesSim

@@ -6,8 +6,9 @@ from tests import golden_utils as gu
 
 
 def oracle_backend(oracle_lib):
-    def make(n, p2_mode, dense, autoreset, seed):
-        o = oracle_lib.Oracle(n, p2_mode=p2_mode, dense_reward=dense, autoreset_mode=autoreset, base_seed=seed)
+    def make(n, p2_mode, dense, autoreset, seed, frame_delay=0):
+        o = oracle_lib.Oracle(n, p2_mode=p2_mode, dense_reward=dense, autoreset_mode=autoreset, base_seed=seed,
+                              frame_delay=frame_delay)
 
         class B:
             def reset(self):
