@@ -8,6 +8,7 @@ ctypes.  Python-side surfaces:
   FootsiesVectorEnv  gymnasium-style VectorEnv over N arenas (drop-in for N x FootsiesEnv)
   FootsiesEnv        single-arena adapter with the reference FootsiesEnv API
   FootsiesSim        the zero-copy handle (torch device tensors in/out)
+  wrappers           vectorized counterparts of the reference's gymnasium wrappers
 """
 from ._abi import MOVE_ID_TO_INDEX, MOVE_INDEX_TO_ID, MOVES  # noqa: F401
 from ._lib import FootsiesError  # noqa: F401
@@ -22,6 +23,10 @@ def __getattr__(name):  # lazy: importing the package must not require torch or 
     if name in ("FootsiesVectorEnv", "FootsiesEnv"):
         from . import vector_env
         return getattr(vector_env, name)
+    if name in ("FootsiesActionCombinationsDiscretized", "FootsiesNormalized", "FootsiesFrameSkipped",
+                "FootsiesStatistics"):
+        from . import wrappers
+        return getattr(wrappers, name)
     raise AttributeError(name)
 
 

@@ -120,6 +120,7 @@ LIB_FUNCTIONS = {
     "fs_create": (C.c_int, [C.POINTER(fs_config), C.POINTER(C.c_void_p)]),
     "fs_reset": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "fs_step_masked": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_n": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(fs_outputs)]),
     "fs_hash_actions": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "fs_outputs_get": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),

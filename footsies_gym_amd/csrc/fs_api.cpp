@@ -265,7 +265,7 @@ FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int
 }
 
 static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2, int flags, uint64_t seed,
-                       const fs_outputs* traj) {
+                       const fs_outputs* traj, const uint8_t* active = nullptr) {
   int rc;
   if ((rc = use_device(h))) return rc;
   const size_t N = (size_t)h->n;
@@ -286,12 +286,18 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
     memcpy(h->h_act, p1, N);
     if (ext) memcpy(h->h_act + N, p2, N);
     HIP_TRY(h, hipMemcpyAsync(h->d_act, h->h_act, ext ? 2 * N : N, hipMemcpyHostToDevice, h->stream));
+    if (active) {
+      memcpy(h->h_mask, active, N);
+      HIP_TRY(h, hipMemcpyAsync(h->d_mask, h->h_mask, N, hipMemcpyHostToDevice, h->stream));
+    }
     HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
     sp.p1 = h->d_act;
     sp.p2 = ext ? h->d_act + N : nullptr;
+    sp.active = active ? h->d_mask : nullptr;
   } else {
     sp.p1 = p1;
     sp.p2 = ext ? p2 : nullptr;
+    sp.active = active;
   }
   if (traj) {
     sp.out = fsk::DevOutputs{traj->guard,          traj->move,           traj->move_frame,  traj->position,
@@ -331,6 +337,18 @@ FS_API int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, in
     return set_err(h, FS_E_INVALID, "fs_step: p2 actions required for FS_P2_EXTERNAL");
   if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
   return step_common(h, 1, p1_act, p2_act, flags, 0, nullptr);
+}
+
+FS_API int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, const uint8_t* active,
+                          int flags) {
+  if (!h) return FS_E_INVALID;
+  if (!p1_act || !active) return set_err(h, FS_E_INVALID, "fs_step_masked: p1 actions and mask required");
+  if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
+    return set_err(h, FS_E_INVALID, "fs_step_masked: p2 actions required for FS_P2_EXTERNAL");
+  if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
+  if (h->cfg.frame_delay > 0)
+    return set_err(h, FS_E_UNSUPPORTED, "fs_step_masked: the delayed-frame queues advance in lockstep");
+  return step_common(h, 1, p1_act, p2_act, flags, 0, nullptr, active);
 }
 
 FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act, uint64_t action_seed,

@@ -45,6 +45,7 @@ struct StepParams {
   DevOutputs out;
   const uint8_t* p1;   // [n][N] or null (hashed)
   const uint8_t* p2;   // [n][N] or null
+  const uint8_t* active;  // [N] or null: single-tick launches skip arenas whose byte is 0
   uint64_t action_seed;
   uint64_t t0;         // global step index of the first tick (hash counter)
   int n_envs;

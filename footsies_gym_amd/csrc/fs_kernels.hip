@@ -1053,6 +1053,9 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   uint32_t next = fetch(0);
   stage_tables();
   if (!active) return;
+  if constexpr (!FUSED) {
+    if (p.active && !p.active[a]) return;  // fs_step_masked: this arena does not tick
+  }
   L.ai = action_info(L.f.act);
   if constexpr (FUSED) {
     const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;

@@ -116,26 +116,36 @@ class FootsiesSim:
                              flags), self._h)
         return self._out
 
-    def step(self, p1, p2=None):
+    def step(self, p1, p2=None, active=None):
         """One env-step of every arena.  Actions: torch uint8 device tensors [N] (fast path) or
-        host arrays ((N,3) bools or (N,) ints)."""
+        host arrays ((N,3) bools or (N,) ints).  active: optional [N] mask -- only those arenas
+        tick (fs_step_masked); the others keep their state and outputs."""
         torch = _torch()
         ext = self.p2_mode == "external"
         if ext and p2 is None:
             raise ValueError("p2 actions are required when p2_mode='external'")
-        on_device = any(isinstance(x, torch.Tensor) and x.is_cuda for x in (p1, p2))
+        on_device = any(isinstance(x, torch.Tensor) and x.is_cuda for x in (p1, p2, active))
         if on_device:  # device path: anything on the host is moved over first
             p1 = _as_u8_device(_to_device(p1, self.device), self.num_envs)
             p2t = _as_u8_device(_to_device(p2, self.device), self.num_envs) if ext else None
-            check(lib().fs_step(self._h, C.c_void_p(p1.data_ptr()),
-                                C.c_void_p(p2t.data_ptr()) if ext else None, _abi.FS_ACT_DEVICE), self._h)
+            q2 = C.c_void_p(p2t.data_ptr()) if ext else None
+            if active is None:
+                check(lib().fs_step(self._h, C.c_void_p(p1.data_ptr()), q2, _abi.FS_ACT_DEVICE), self._h)
+            else:
+                m = torch.as_tensor(active, device=self.device).reshape(self.num_envs).to(torch.uint8).contiguous()
+                check(lib().fs_step_masked(self._h, C.c_void_p(p1.data_ptr()), q2, C.c_void_p(m.data_ptr()),
+                                           _abi.FS_ACT_DEVICE), self._h)
         else:
             a1 = np.ascontiguousarray(encode_actions(_host(p1)))
             a2 = np.ascontiguousarray(encode_actions(_host(p2))) if ext else None
             if a1.shape[0] != self.num_envs or (a2 is not None and a2.shape[0] != self.num_envs):
                 raise ValueError("expected %d actions" % self.num_envs)
-            check(lib().fs_step(self._h, a1.ctypes.data, None if a2 is None else a2.ctypes.data,
-                                _abi.FS_ACT_HOST), self._h)
+            q2 = None if a2 is None else a2.ctypes.data
+            if active is None:
+                check(lib().fs_step(self._h, a1.ctypes.data, q2, _abi.FS_ACT_HOST), self._h)
+            else:
+                m = np.ascontiguousarray(np.asarray(active).reshape(self.num_envs), dtype=np.uint8)
+                check(lib().fs_step_masked(self._h, a1.ctypes.data, q2, m.ctypes.data, _abi.FS_ACT_HOST), self._h)
         return self._out
 
     def step_n(self, n, p1=None, p2=None, action_seed=0, trajectory=None):

@@ -124,3 +124,25 @@ def batch_observation_space(num_envs):
 
 def batch_action_space(num_envs):
     return MultiBinary((num_envs, 3))
+
+
+def normalized_observation_space(normalize_guard=True):
+    """FootsiesNormalized.observation_space (normalization.py:24-29)."""
+    s = single_observation_space()
+    d = {k: s[k] for k in ("guard", "move", "move_frame", "position")}
+    if normalize_guard:
+        d["guard"] = Box(low=0.0, high=1.0, shape=(2,))
+    d["move_frame"] = Box(low=0.0, high=1.0, shape=(2,))
+    d["position"] = Box(low=-1.0, high=1.0, shape=(2,))
+    return Dict(d)
+
+
+def frame_skipped_observation_space(wrapped):
+    """FootsiesFrameSkipped.observation_space (frame_skip.py:18-33): P2's move_frame only."""
+    mf = wrapped["move_frame"]
+    return Dict({
+        "guard": wrapped["guard"],
+        "move": wrapped["move"],
+        "move_frame": Box(low=float(mf.low[1]), high=float(mf.high[1]), shape=(1,)),
+        "position": wrapped["position"],
+    })

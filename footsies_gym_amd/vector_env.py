@@ -139,6 +139,28 @@ class FootsiesVectorEnv:
         self._last = (obs, info)
         return obs, rew, term, trunc, info
 
+    def step_masked(self, actions, active):
+        """Step only the arenas where ``active`` is true (fs_step_masked), as separate
+        FootsiesEnv instances that are stepped at different times.  The returned batch
+        holds, for inactive arenas, their previous observation with reward 0 and not
+        terminated (numpy output)."""
+        p2 = None
+        if self.sim.p2_mode == "external":
+            p2 = self._opponent(*self._last) if self._last is not None else np.zeros(self.num_envs, np.uint8)
+        out = self.sim.step(actions, p2, active=active)
+        if self.output == "torch":
+            obs = {k: out[k] for k in ("guard", "move", "move_frame", "position")}
+            self._last = (obs, out)
+            return obs, out["reward"], out["terminated"], out["truncated"], out
+        host = self.sim.outputs_numpy()
+        idle = ~np.asarray(active, dtype=bool).reshape(self.num_envs)
+        host["reward"][idle] = 0.0
+        host["terminated"][idle] = 0
+        host["truncated"][idle] = 0
+        obs, rew, term, trunc, info = step_result_from_outputs(host, self.autoreset_mode)
+        self._last = (obs, info)
+        return obs, rew, term, trunc, info
+
     def close(self):
         self.sim.close()
 

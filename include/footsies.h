@@ -190,6 +190,13 @@ int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int flags)
  * flags: FS_ACT_HOST or FS_ACT_DEVICE for where the action arrays live. */
 int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags);
 
+/* fs_step for the arenas whose active[i] != 0 only; the others keep their state
+ * and their outputs (which then still hold their previous step's values).  This
+ * lets arenas advance at their own pace, as N separate FootsiesEnv instances do
+ * under a frame-skipping wrapper (wrappers/frame_skip.py:63-80).  active lives
+ * where flags says the actions do.  FS_E_UNSUPPORTED with frame_delay > 0. */
+int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, const uint8_t* active, int flags);
+
 /* n Fight ticks in one kernel launch (fused rollout).  Actions: device arrays
  * [n][N], or NULL to draw them on device from the counter-based hash
  * a = splitmix64(action_seed ^ env*0x9E3779B97F4A7C15 ^ (t << 1 | player)) & 7

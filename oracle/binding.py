@@ -36,6 +36,7 @@ def lib():
         L.or_create.argtypes = [C.POINTER(abi.fs_config), C.POINTER(C.c_void_p)]
         L.or_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.or_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_step_masked.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_step_n_hashed.argtypes = [C.c_void_p, C.c_int, C.c_uint64]
         L.or_outputs_get.argtypes = [C.c_void_p, C.POINTER(abi.fs_outputs)]
         L.or_get_env_state.argtypes = [C.c_void_p, C.POINTER(abi.fs_env_state)]
@@ -99,10 +100,15 @@ class Oracle:
         assert rc == 0, rc
         return self.outputs()
 
-    def step(self, p1, p2=None):
+    def step(self, p1, p2=None, active=None):
         p1 = np.ascontiguousarray(p1, dtype=np.uint8)
         p2 = None if p2 is None else np.ascontiguousarray(p2, dtype=np.uint8)
-        rc = lib().or_step(self.h, p1.ctypes.data, None if p2 is None else p2.ctypes.data)
+        q2 = None if p2 is None else p2.ctypes.data
+        if active is None:
+            rc = lib().or_step(self.h, p1.ctypes.data, q2)
+        else:
+            m = np.ascontiguousarray(active, dtype=np.uint8)
+            rc = lib().or_step_masked(self.h, p1.ctypes.data, q2, m.ctypes.data)
         assert rc == 0, rc
         return self.outputs()
 

@@ -1196,6 +1196,19 @@ OR_EXPORT int or_step(or_handle C, const uint8_t* p1, const uint8_t* p2) {
   return FS_OK;
 }
 
+/* fs_step_masked: only arenas with active[i] != 0 run FootsiesEnv.step; the others are
+   separate environments that were not stepped (state and outputs untouched) */
+OR_EXPORT int or_step_masked(or_handle C, const uint8_t* p1, const uint8_t* p2, const uint8_t* active) {
+  if (!C || !p1 || !active) return FS_E_INVALID;
+  if (C->cfg.p2_mode == FS_P2_EXTERNAL && !p2) return FS_E_INVALID;
+  if (C->cfg.frame_delay > 0) return FS_E_UNSUPPORTED;
+#pragma omp parallel for schedule(static) if (C->n >= 1024)
+  for (int i = 0; i < C->n; i++)
+    if (active[i]) fe_step_arena(C, i, p1[i], p2 ? p2[i] : 0);
+  C->steps++;
+  return FS_OK;
+}
+
 static inline uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;

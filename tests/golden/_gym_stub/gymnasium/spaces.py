@@ -1,3 +1,6 @@
+import numpy as np
+
+
 class Space:
     def __init__(self, *a, **k):
         self.args, self.kwargs = a, k
@@ -16,7 +19,11 @@ class MultiDiscrete(Space):
 
 
 class Box(Space):
-    pass
+    def __init__(self, low, high, shape=None, dtype=np.float32, **k):
+        super().__init__(low, high, shape=shape, dtype=dtype, **k)
+        shape = shape if shape is not None else np.shape(low)
+        self.low = np.full(shape, low, dtype=dtype)
+        self.high = np.full(shape, high, dtype=dtype)
 
 
 class MultiBinary(Space):

@@ -6,6 +6,7 @@ import pytest
 from footsies_gym_amd import _abi
 from tests import golden_utils as gu
 from tests import kat_scenarios as kat
+from tests import wrapper_replay as wr
 from tests.gpu_backend import SimBackend, make
 from tests.parity_utils import compare_outputs, compare_states
 
@@ -81,6 +82,32 @@ def test_frame_delay_paths_match_oracle(oracle_lib, autoreset):
     for t in range(D + 3):
         b.step(h1[t], h2[t])
         compare_outputs(ora.step(h1[t], h2[t]), b.outputs_numpy(), step=T + t)
+
+
+@pytest.mark.parametrize("p2", ["bot", "external"])
+def test_step_masked_matches_oracle(oracle_lib, p2):
+    """fs_step_masked: only active arenas tick; the others keep state and outputs."""
+    from footsies_gym_amd.simulator import FootsiesSim
+    N, T = 999, 300
+    p2m = _abi.FS_P2_BOT if p2 == "bot" else _abi.FS_P2_EXTERNAL
+    s = FootsiesSim(N, p2_mode=p2, seed=21)
+    ora = oracle_lib.Oracle(N, p2_mode=p2m, base_seed=21)
+    rng = np.random.default_rng(5)
+    for t in range(T):
+        a1 = rng.integers(0, 8, N).astype(np.uint8)
+        a2 = rng.integers(0, 8, N).astype(np.uint8) if p2 == "external" else None
+        active = rng.random(N) < (0.3 if t % 2 else 0.9)
+        s.step(a1, a2, active=active)
+        exp = ora.step(a1, a2, active=active.astype(np.uint8))
+        compare_outputs(exp, s.outputs_numpy(), step=t)
+    compare_states(ora.state(), s.get_state())
+
+
+@pytest.mark.parametrize("name", wr.CASES)
+def test_wrappers_match_reference_gpu(name):
+    from footsies_gym_amd.vector_env import FootsiesVectorEnv
+    wr.replay(name, lambda n, dense, seed: FootsiesVectorEnv(n, opponent=None, dense_reward=dense, seed=seed,
+                                                             autoreset_mode="next_step"))
 
 
 def test_hashed_actions_match_host_stream(oracle_lib):
