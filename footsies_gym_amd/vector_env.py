@@ -15,7 +15,7 @@ Differences from the reference, by design:
 """
 import numpy as np
 
-from . import _abi
+from . import _abi, battle_state
 from . import spaces as sp
 from .simulator import FootsiesSim, decode_actions, encode_actions
 
@@ -173,6 +173,18 @@ class FootsiesVectorEnv:
         """STATE_LOAD (BC:153-156)."""
         self.sim.set_state(state)
 
+    def save_battle_state_json(self, arena=0):
+        """STATE_SAVE of one arena in the reference's BattleState JSON (battle_state.py)."""
+        return battle_state.dumps(battle_state.battle_state(self.sim.get_state(), arena))
+
+    def load_battle_state_json(self, state, arena=0):
+        """STATE_LOAD of one arena from BattleState JSON text, a dict or a FootsiesBattleState;
+        the arena keeps what BattleState does not carry (bot RNG, recording, reward sum)."""
+        if isinstance(state, battle_state.FootsiesBattleState):
+            state = state.to_dict()
+        states = self.sim.get_state()
+        self.sim.set_state(battle_state.load_into(states, arena, state))
+
     @property
     def most_recent_observation(self):
         return None if self._last is None else self._last[0]
@@ -235,6 +247,14 @@ class FootsiesEnv:
 
     def close(self):
         self.venv.close()
+
+    def save_battle_state(self):
+        """FE:466-471: the game's BattleState (STATE_SAVE)."""
+        return battle_state.FootsiesBattleState.from_json(self.venv.save_battle_state_json(0))
+
+    def load_battle_state(self, state):
+        """FE:473-478: STATE_LOAD of a FootsiesBattleState."""
+        self.venv.load_battle_state_json(state, 0)
 
     @property
     def most_recent_observation(self):

@@ -41,6 +41,7 @@ def lib():
         L.or_outputs_get.argtypes = [C.c_void_p, C.POINTER(abi.fs_outputs)]
         L.or_get_env_state.argtypes = [C.c_void_p, C.POINTER(abi.fs_env_state)]
         L.or_get_state.argtypes = [C.c_void_p, C.POINTER(abi.fs_arena_state)]
+        L.or_set_state.argtypes = [C.c_void_p, C.POINTER(abi.fs_arena_state)]
         L.or_destroy.argtypes = [C.c_void_p]
         L.or_hash_action.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int]
         L.or_hash_action.restype = C.c_uint8
@@ -125,6 +126,11 @@ class Oracle:
         arr = (abi.fs_arena_state * self.n)()
         lib().or_get_state(self.h, arr)
         return np.ctypeslib.as_array(arr).copy()
+
+    def set_state(self, states):
+        arr = (abi.fs_arena_state * self.n)()
+        np.ctypeslib.as_array(arr)[:] = states
+        return lib().or_set_state(self.h, arr)
 
     def close(self):
         if self.h:

@@ -1313,6 +1313,63 @@ OR_EXPORT int or_get_state(or_handle C, fs_arena_state* out) {
   return FS_OK;
 }
 
+/* STATE_LOAD of the canonical state (fs_set_state).  The 180-deep histories are rebuilt
+   from what fs_arena_state carries -- directions of input[0..15], Attack over the held run
+   input[0..hold-1] -- with zeros beyond; inputDown / inputUp follow from input (F:182-184).
+   Boxes and velocity_x are left for the next UpdateBoxes / UpdateMovement to set.  A
+   pending terminal arena resumes in KO with its timer at 0 (BC:303-306).  The scripted
+   bot's queues and FightState ring are not rebuilt here: FS_E_UNSUPPORTED for FS_P2_BOT. */
+OR_EXPORT int or_set_state(or_handle C, const fs_arena_state* in) {
+  if (!C || !in) return FS_E_INVALID;
+  if (C->cfg.p2_mode == FS_P2_BOT) return FS_E_UNSUPPORTED;
+  for (int i = 0; i < C->n; i++) {
+    arena_t* A = &C->a[i];
+    const fs_arena_state* s = &in[i];
+    for (int k = 0; k < 2; k++) {
+      fighter_t* f = &A->f[k];
+      const fs_fighter_state* g = &s->f[k];
+      f->pos_x = g->position_x;
+      f->pos_y = 0.0f;
+      f->action_id = g->action_id;
+      f->action_frame = g->action_frame;
+      f->hit_count = g->hit_count;
+      f->hitstun = g->hitstun;
+      f->vital = g->vital;
+      f->guard = g->guard;
+      f->buffer_action_id = g->buffer_action_id;
+      f->reserve_damage_action_id = g->reserve_action_id;
+      clear_input(f);
+      f->head = 0;
+      for (int j = 0; j < OR_INPUT_RECORD_FRAME; j++) {
+        int v = j < 16 ? (int)((g->input_dir_history >> (2 * j)) & 3u) : 0;
+        if (j < g->attack_hold) v |= IN_ATTACK;
+        f->in[j] = v;
+      }
+      for (int j = 0; j < OR_INPUT_RECORD_FRAME; j++) {
+        int next = j + 1 < OR_INPUT_RECORD_FRAME ? f->in[j + 1] : 0;
+        f->in_down[j] = (f->in[j] ^ next) & f->in[j];
+        f->in_up[j] = (f->in[j] ^ next) & ~f->in[j];
+      }
+      f->is_input_backward = g->is_input_backward;
+      f->is_reserve_proximity_guard = g->is_reserve_proximity_guard;
+      f->has_won = g->has_won;
+    }
+    A->frame_count = s->frame_count;
+    A->rec_idx = (uint32_t)s->recording_count;
+    A->rec_last[0] = s->recording_last[0];
+    A->rec_last[1] = s->recording_last[1];
+    A->actor_in[0] = s->actor_input[0];
+    A->actor_in[1] = s->actor_input[1];
+    A->reset_pending = s->reset_pending;
+    A->has_terminated = s->has_terminated;
+    A->cum_reward = s->cumulative_reward;
+    A->round_state = s->reset_pending ? RS_KO : RS_FIGHT;
+    A->timer = 0.0f;
+    A->cur_state = get_environment_state(A);
+  }
+  return FS_OK;
+}
+
 OR_EXPORT void or_set_threads(int n) {
 #ifdef _OPENMP
   if (n > 0) omp_set_num_threads(n);

@@ -110,6 +110,48 @@ def test_wrappers_match_reference_gpu(name):
                                                              autoreset_mode="next_step"))
 
 
+def test_battle_state_json_into_gpu_continues_like_oracle(oracle_lib):
+    """Oracle arenas mid-episode -> BattleState JSON -> loaded into GPU arenas (which keep
+    their own non-BattleState fields, copied from the oracle first) -> identical futures."""
+    from footsies_gym_amd import battle_state as B
+    from footsies_gym_amd.vector_env import FootsiesVectorEnv
+    n = 300
+    rng = np.random.default_rng(8)
+    ora = oracle_lib.Oracle(n, p2_mode=_abi.FS_P2_EXTERNAL, base_seed=2)
+    for _ in range(210):
+        ora.step(rng.integers(0, 8, n), rng.integers(0, 8, n))
+    snap = ora.state()
+    venv = FootsiesVectorEnv(n, opponent=lambda o, i: np.zeros(n, np.uint8), seed=2)
+    venv.load_battle_state(snap)  # the non-BattleState fields (recording, reward sum, ...)
+    base = venv.save_battle_state()
+    base["f"]["action_id"] = 0
+    base["f"]["position_x"] = 0.0
+    venv.load_battle_state(base)
+    for i in range(n):
+        venv.load_battle_state_json(B.dumps(B.battle_state(snap, i)), arena=i)
+    compare_states(snap, venv.save_battle_state())
+    for t in range(300):
+        a1, a2 = rng.integers(0, 8, n).astype(np.uint8), rng.integers(0, 8, n).astype(np.uint8)
+        venv.sim.step(a1, a2)
+        compare_outputs(ora.step(a1, a2), venv.sim.outputs_numpy(), step=t)
+    venv.close()
+
+
+def test_single_env_battle_state_roundtrip():
+    from footsies_gym_amd.vector_env import FootsiesEnv
+    env = FootsiesEnv(opponent=lambda o, i: (False, True, False))
+    env.reset()
+    for t in range(77):
+        env.step((t % 3 == 0, False, t % 5 == 0))
+    saved = env.save_battle_state()
+    after = [env.step((False, t % 2 == 0, False)) for t in range(40)]
+    env.load_battle_state(saved)
+    again = [env.step((False, t % 2 == 0, False)) for t in range(40)]
+    for (o1, r1, d1, _, i1), (o2, r2, d2, _, i2) in zip(after, again):
+        assert o1 == o2 and r1 == r2 and d1 == d2 and i1["frame"] == i2["frame"]
+    env.close()
+
+
 def test_hashed_actions_match_host_stream(oracle_lib):
     """fs_hash_actions / in-kernel hashing == the splitmix64 stream of SURVEY.md §8(d)."""
     from footsies_gym_amd.simulator import FootsiesSim
