@@ -6,6 +6,7 @@ import pytest
 from footsies_gym_amd import _abi
 from tests import golden_utils as gu
 from tests import kat_scenarios as kat
+from tests import wire_client, wire_replay
 from tests import wrapper_replay as wr
 from tests.gpu_backend import SimBackend, make
 from tests.parity_utils import compare_outputs, compare_states
@@ -150,6 +151,55 @@ def test_single_env_battle_state_roundtrip():
     for (o1, r1, d1, _, i1), (o2, r2, d2, _, i2) in zip(after, again):
         assert o1 == o2 and r1 == r2 and d1 == d2 and i1["frame"] == i2["frame"]
     env.close()
+
+
+@pytest.mark.parametrize("name", wire_replay.CASES)
+def test_wire_server_gpu_replays_reference_client_traffic(name):
+    """The reference client's recorded traffic, served by the GPU-backed game server."""
+    from footsies_gym_amd.server import SimBackend
+    assert wire_replay.replay(name, lambda p2_bot, seed: SimBackend(p2_bot=p2_bot, seed=seed)) > 1000
+
+
+def test_wire_server_p2_bot_toggle():
+    """P2_BOT switches P2 between the remote actor and the in-game bot mid-battle."""
+    import json
+    import struct
+    import threading
+    from footsies_gym_amd.server import FootsiesServer
+    srv = FootsiesServer("127.0.0.1", 0, 0, 0, seed=5)
+    th = threading.Thread(target=srv.serve, daemon=True)
+    th.start()
+    p1 = wire_client.connect("127.0.0.1", srv.ports["p1"])
+    rc = wire_client.connect("127.0.0.1", srv.ports["rc"])
+    p2 = wire_client.connect("127.0.0.1", srv.ports["p2"])
+
+    def state():
+        return json.loads(wire_client.recv_message(p1)[4:])
+
+    def command(c, v=""):
+        m = json.dumps({"command": c, "value": v}).encode()
+        rc.sendall(struct.pack("!I", len(m)) + m)
+
+    s = state()
+    assert s["globalFrame"] == -1
+    p2_moves = {"remote": set(), "bot": set(), "remote again": set()}
+    for phase, remote in (("remote", True), ("bot", False), ("remote again", True)):
+        command(4, str(not remote))
+        for t in range(150):
+            p1.sendall(bytes([0, 0, 0]))
+            if remote:
+                p2.sendall(bytes([0, 0, 0]))
+            s = state()
+            if s["p1Vital"] == 0 or s["p2Vital"] == 0:
+                s = state()  # the next episode's state(-1)
+            p2_moves[phase].add(s["p2Move"])
+    assert p2_moves["remote"] <= {0}  # an idle remote P2 only stands
+    assert len(p2_moves["bot"]) > 1    # the bot moves
+    assert 0 in p2_moves["remote again"]
+    for x in (p1, rc, p2):
+        x.close()
+    srv.stop()
+    th.join(timeout=30)
 
 
 def test_hashed_actions_match_host_stream(oracle_lib):
