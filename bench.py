@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-samples", type=int, default=50, help="launches timed back-to-back for roofline")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C2 bot-opponent and C5 policy-loop rates")
     return ap.parse_args()
 
 
@@ -69,6 +70,56 @@ def cpu_baseline(envs, seconds, seed):
     return {"value": envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": "%d arenas x %d steps, self-play splitmix64 actions, oracle/liboracle.so (OpenMP %d threads), "
                       "%.1f s" % (envs, steps, threads, dt)}
+
+
+def bot_mode_rate(torch, N, K, W, chunk, seed, device):
+    """Config C2's opponent at the C3 size: P1 random (HBM), P2 the in-kernel BattleAI, fused."""
+    import ctypes as C
+    from footsies_gym_amd import _abi
+    from footsies_gym_amd._lib import check, lib
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
+    p1, _ = sim.hash_actions(W + K, seed=seed, p2=False)
+    traj = sim.alloc_trajectory(chunk)
+    td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+
+    def run(k0, n):
+        k = k0
+        while k < k0 + n:
+            m = min(chunk, k0 + n - k)
+            check(lib().fs_step_n(sim.handle, m, C.c_void_p(p1.data_ptr() + k * N), None, 0, C.byref(td)), sim.handle)
+            k += m
+    run(0, W)
+    torch.cuda.synchronize(device)
+    t = time.perf_counter()
+    run(W, K)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t
+    sim.close()
+    return {"value": N * K / dt, "ms_per_step": 1e3 * dt / K, "kernel": "fsk::k_step_n<0, 1>",
+            "config": "C2 opponent: P1 random actions, P2 = in-kernel BattleAI, %d arenas" % N}
+
+
+def policy_loop_rate(torch, N, steps, device):
+    """Config C5: a 2x64 MLP actor samples P1's action from the outputs every step (P2 = bot);
+    blocks of steps are captured into one HIP graph and replayed."""
+    from footsies_gym_amd.rollout import PolicyRollout, make_actor
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
+    ro = PolicyRollout(sim, make_actor(device=torch.device("cuda", device)))
+    block = 25
+    ro.capture(block)
+    ro.replay(2)
+    torch.cuda.synchronize(device)
+    reps = max(1, steps // block)
+    t = time.perf_counter()
+    ro.replay(reps)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t
+    sim.close()
+    return {"value": N * reps * block / dt, "ms_per_step": 1e3 * dt / (reps * block), "graph_steps": block,
+            "config": "C5: %d arenas, Linear(8,64)-tanh-Linear(64,64)-tanh-Linear(64,8) actor, Gumbel-max "
+                      "sampling + log-prob, fs_step per step, P2 = bot, HIP graph replay" % N}
 
 
 def pmc_traffic(kernel, envs, ticks):
@@ -231,6 +282,12 @@ def main():
         "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
                                    "note": "fs_step with FS_ACT_HOST (PCIe-inclusive action hand-over)"},
     }
+    if world == 1 and not args.no_extras:
+        out["p2_bot_mode"] = bot_mode_rate(torch, N, K, W, chunk, args.seed, local)
+        try:
+            out["policy_loop"] = policy_loop_rate(torch, N, min(K, 1000), local)
+        except Exception as e:  # reported, never fatal to the headline measurement
+            out["policy_loop"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)
     if rank == 0:

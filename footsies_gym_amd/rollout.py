@@ -1,0 +1,105 @@
+"""On-device rollouts with a policy in the loop.
+
+Every step: the simulator's outputs (device tensors, written in place by libfootsies.so)
+-> features -> a 2x64 MLP actor -> a sampled action per arena (Gumbel-max, with its
+log-probability for PPO) -> fs_step with device actions.  Nothing leaves the GPU and
+nothing synchronises, so a block of steps is captured once into a HIP graph and
+replayed: the loop then costs graph launches, not the ~20 kernel launches per step.
+
+Graph replays do not advance the handle's host-side step counter (fs_steps_taken), which
+only the hashed-action stream and frame_delay > 0 read; use eager steps for those.
+"""
+import ctypes as C
+
+from . import _abi
+from ._lib import check, lib
+
+N_FEATURES = 8
+N_ACTIONS = 8  # (left, right, attack) combinations, FootsiesActionCombinationsDiscretized
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def obs_features(out):
+    """[N, 8] float32: guard / 3, move / 16, move_frame / 55, position / 4.6 for P1 and P2
+    (the reference's normalisation constants, wrappers/normalization.py)."""
+    torch = _torch()
+    return torch.cat([out["guard"].float() / 3.0, out["move"].float() / 16.0, out["move_frame"] / 55.0,
+                      out["position"] / 4.6], dim=1)
+
+
+def make_actor(hidden=64, device=None, seed=0):
+    """The C5 actor: Linear(8, 64) - tanh - Linear(64, 64) - tanh - Linear(64, 8), random init."""
+    torch = _torch()
+    g = torch.Generator().manual_seed(seed)
+    nn = torch.nn
+    net = nn.Sequential(nn.Linear(N_FEATURES, hidden), nn.Tanh(), nn.Linear(hidden, hidden), nn.Tanh(),
+                        nn.Linear(hidden, N_ACTIONS))
+    with torch.no_grad():
+        for p in net.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.3)
+    return net.to(device)
+
+
+class PolicyRollout:
+    """Steps `sim` (a FootsiesSim) with actions sampled from `actor`; P2 is whatever the
+    handle was created with (bot, noop, or `p2_actions` for external)."""
+
+    def __init__(self, sim, actor, p2_actions=None):
+        torch = _torch()
+        self.sim, self.actor = sim, actor
+        n = sim.num_envs
+        dev = sim.device
+        self.action = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.logp = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.p2 = p2_actions if p2_actions is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.graph = None
+        self.graph_steps = 0
+        self.action_log = None  # [graph steps][N] actions of the last replay when capture(log=True)
+
+    def _step(self, log_row=None):
+        torch = _torch()
+        out = self.sim.outputs()
+        with torch.no_grad():
+            logits = self.actor(obs_features(out))
+            u = torch.rand_like(logits).clamp_(1e-9, 1.0)
+            a = torch.argmax(logits - torch.log(-torch.log(u)), dim=1)
+            self.logp.copy_(torch.log_softmax(logits, dim=1).gather(1, a[:, None])[:, 0])
+            self.action.copy_(a.to(torch.uint8))
+            if log_row is not None:
+                log_row.copy_(self.action)
+        check(lib().fs_step(self.sim.handle, C.c_void_p(self.action.data_ptr()), C.c_void_p(self.p2.data_ptr()),
+                            _abi.FS_ACT_DEVICE), self.sim.handle)
+
+    def step_eager(self, n=1):
+        for _ in range(n):
+            self._step()
+
+    def capture(self, steps, warmup=2, log=False):
+        """Capture `steps` policy+simulator steps into one HIP graph on a private stream, after
+        `warmup` eager steps there (library / BLAS handles and the allocator settle outside the
+        capture).  Returns the warm-up steps' actions ([warmup][N], host) so they can be replayed."""
+        torch = _torch()
+        stream = torch.cuda.Stream(device=self.sim.device)
+        self.sim.use_torch_stream(stream)  # the library issues its kernels on the capture stream
+        warm = []
+        with torch.cuda.stream(stream):
+            for _ in range(warmup):
+                self._step()
+                warm.append(self.action.cpu())
+        stream.synchronize()
+        if log:
+            self.action_log = torch.zeros((steps, self.sim.num_envs), dtype=torch.uint8, device=self.sim.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for i in range(steps):
+                self._step(self.action_log[i] if log else None)
+        self.graph, self.graph_steps, self.stream = g, steps, stream
+        return warm
+
+    def replay(self, times=1):
+        for _ in range(times):
+            self.graph.replay()

@@ -202,6 +202,28 @@ def test_wire_server_p2_bot_toggle():
     th.join(timeout=30)
 
 
+def test_policy_rollout_graph_matches_oracle(oracle_lib):
+    """C5 loop: MLP actor + fs_step captured in a HIP graph; the actions it sampled, replayed
+    through the oracle (same bot seeds), give the same outputs and state."""
+    import torch
+    from footsies_gym_amd.rollout import PolicyRollout, make_actor
+    from footsies_gym_amd.simulator import FootsiesSim
+    N = 2000
+    sim = FootsiesSim(N, p2_mode="bot", seed=13)
+    ora = oracle_lib.Oracle(N, p2_mode=_abi.FS_P2_BOT, base_seed=13)
+    ro = PolicyRollout(sim, make_actor(device=torch.device("cuda", 0), seed=4))
+    for a in ro.capture(7, warmup=3, log=True):
+        ora.step(a.numpy())
+    for _ in range(4):
+        ro.replay()
+        torch.cuda.synchronize()
+        for a in ro.action_log.cpu().numpy():
+            exp = ora.step(a)
+    assert len(np.unique(ro.action_log.cpu().numpy())) == 8
+    compare_outputs(exp, sim.outputs_numpy())
+    compare_states(ora.state(), sim.get_state())
+
+
 def test_hashed_actions_match_host_stream(oracle_lib):
     """fs_hash_actions / in-kernel hashing == the splitmix64 stream of SURVEY.md §8(d)."""
     from footsies_gym_amd.simulator import FootsiesSim
