@@ -269,7 +269,6 @@ def main(argv=None):
     ap.add_argument("--p2-address", default=None)
     ap.add_argument("--p2-port", type=int, default=None)
     ap.add_argument("--p2-no-state", action="store_true")
-    ap.add_argument("--sparse-reward", action="store_true", help="unused by the protocol; kept for symmetry")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
     # accepted for command-line compatibility with the game binary; no effect here
@@ -278,7 +277,11 @@ def main(argv=None):
         ap.add_argument(flag, action="store_true")
     ap.add_argument("--fast-forward-speed", type=float, default=None)
     ap.add_argument("-logFile", default=None)
+    for flag in ("--p1-bot", "--p1-spectator", "--p1-player", "--p2-player", "--p2-spectator", "--p1-no-state"):
+        ap.add_argument(flag, action="store_true")
     a = ap.parse_args(argv)
+    if a.p1_bot or a.p1_player or a.p2_player or a.p1_spectator or a.p2_spectator or a.p1_no_state:
+        ap.error("only the training setup is served: P1 remote agent, P2 bot or remote agent")
     srv = FootsiesServer(a.p1_address, a.p1_port, a.remote_control_port, a.p2_port, a.p2_no_state,
                          p2_bot=True if a.p2_bot else None, device=a.device, seed=a.seed,
                          remote_control_address=a.remote_control_address, p2_address=a.p2_address)

@@ -224,6 +224,50 @@ def test_policy_rollout_graph_matches_oracle(oracle_lib):
     compare_states(ora.state(), sim.get_state())
 
 
+def test_game_binary_stand_in_with_reference_command_line():
+    """bin/FOOTSIES started with the argument list FootsiesEnv._instantiate_game builds
+    (FE:193-259, bot P2, no render) serves the same frames as a one-arena FootsiesSim."""
+    import json
+    import os
+    import socket
+    import subprocess
+    from footsies_gym_amd.server import env_state_json
+    from footsies_gym_amd.simulator import FootsiesSim
+    ports = []
+    for _ in range(2):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            ports.append(s.getsockname()[1])
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = [os.path.join(root, "bin", "FOOTSIES"), "--mute", "--training", "--p1-address", "127.0.0.1", "--p1-port",
+            str(ports[0]), "--remote-control-address", "127.0.0.1", "--remote-control-port", str(ports[1]),
+            "-force-gfx-direct", "-batchmode", "-nographics", "--fast-forward", "--fast-forward-speed", "6.0",
+            "--synced-non-blocking", "--p2-bot", "-nolog"]
+    proc = subprocess.Popen(args, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        p1 = wire_client.connect("127.0.0.1", ports[0], timeout=120)
+        rc = wire_client.connect("127.0.0.1", ports[1], timeout=120)
+        ref = FootsiesSim(1, p2_mode="bot", autoreset_mode="next_step", seed=0)
+        got = wire_client.recv_message(p1)[4:].decode()
+        assert got == env_state_json(ref.env_state()[0])
+        rng = np.random.default_rng(3)
+        for t in range(400):
+            a = rng.integers(0, 2, 3)
+            p1.sendall(bytes(int(x) for x in a))
+            ref.step(np.array([a[0] | a[1] << 1 | a[2] << 2], np.uint8))
+            assert wire_client.recv_message(p1)[4:].decode() == env_state_json(ref.env_state()[0]), t
+            if ref.outputs_numpy()["terminated"][0]:
+                ref.reset()
+                assert json.loads(wire_client.recv_message(p1)[4:])["globalFrame"] == -1
+        p1.close()
+        rc.close()
+        assert proc.wait(timeout=60) == 0, proc.stderr.read()
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+            proc.wait()
+
+
 def test_hashed_actions_match_host_stream(oracle_lib):
     """fs_hash_actions / in-kernel hashing == the splitmix64 stream of SURVEY.md §8(d)."""
     from footsies_gym_amd.simulator import FootsiesSim
