@@ -8,7 +8,8 @@ import os
 
 from . import _abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfootsies.so")
+# FOOTSIES_LIB overrides the in-tree library (kernel experiments, tools/kernel_variants.py)
+LIB_PATH = os.environ.get("FOOTSIES_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfootsies.so")
 
 
 class FootsiesError(RuntimeError):
