@@ -284,15 +284,13 @@ __device__ __forceinline__ InputEval update_input(Fighter& f, uint32_t in, int k
   const uint32_t B = old_hist & 0xFFFFu, F = old_hist >> 16, E = B | F;
   const uint32_t win = (1u << (kDashAllowFrame - 1)) - 1u;
   const uint32_t e8 = E & win;
-  e.fdash = false;
-  e.bdash = false;
-  if (e8) {
-    const int j = __builtin_ctz(e8);  // first i in 1..8 with any direction: i = j + 1
-    const bool neutral = ((~E >> (j + 1)) & win) != 0;  // some input[i+1 .. i+8] with neither direction
-    const bool isF = (F >> j) & 1, isB = (B >> j) & 1;
-    e.fdash = (r0 & 2) && !(r1 & 2) && !isB && isF && neutral;
-    e.bdash = (r0 & 1) && !(r1 & 1) && !isF && isB && neutral;
-  }
+  // branch-free: j = first i - 1 in 1..8 with any direction (8 when none, then gated off)
+  const int j = __builtin_ctz(e8 | (1u << (kDashAllowFrame - 1)));
+  const bool neutral = ((~E >> (j + 1)) & win) != 0;  // some input[i+1 .. i+8] with neither direction
+  const bool isF = (F >> j) & 1, isB = (B >> j) & 1;
+  const bool found = e8 != 0;
+  e.fdash = found & ((r0 & 2) != 0) & ((r1 & 2) == 0) & !isB & isF & neutral;
+  e.bdash = found & ((r0 & 1) != 0) & ((r1 & 1) == 0) & !isF & isB & neutral;
   return e;
 }
 
@@ -320,25 +318,6 @@ __device__ __forceinline__ uint32_t ai_cancel_mask(AInfo i) { return i.z; }
 __device__ __forceinline__ int ai_rec0(AInfo i) { return (int)i.w; }
 static_assert(sizeof(ActionInfo) == 16, "ActionInfo must be 16 bytes");
 
-// RequestAction (F:472-510), branch-free.  `ai` is the ActionInfo of f.act (kept
-// current across a chain of requests), `an` the one of the requested action `a`,
-// `valid` = false turns the call into a no-op.  The cancel windows of an action
-// are one frame range with one target mask (asserted by tools/gen_tables.py); a
-// buffer or execute window listing `a` leaves bufferActionID = a.
-__device__ __forceinline__ void request_action(Fighter& f, AInfo& ai, int a, AInfo an, bool valid) {
-  const bool ended = f.frame >= ai_frame_count(ai);
-  const bool same = f.act == a;
-  const bool take = valid & (ended | (!same & ai_always_cancel(ai)));
-  const bool buffer = valid & !take & !same & (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai)) &
-                      (((ai_cancel_mask(ai) >> a) & 1u) != 0);
-  f.act = take ? a : f.act;
-  f.frame = take ? 0 : f.frame;
-  f.hits = take ? 0 : f.hits;
-  f.rsv = take ? NONE : f.rsv;
-  f.buf = take ? NONE : (buffer ? a : f.buf);
-  ai = take ? an : ai;
-}
-
 // IncrementActionFrame (F:140-166); `ai` = ActionInfo of f.act
 __device__ __forceinline__ void increment_action_frame(Fighter& f, AInfo ai) {
   const bool stunned = f.stun > 0;
@@ -349,14 +328,58 @@ __device__ __forceinline__ void increment_action_frame(Fighter& f, AInfo ai) {
   f.frame = stunned ? f.frame : looped;
 }
 
-// UpdateActionRequest (F:201-286).  Every request target is decided from the inputs
-// and the state before the first request, so the four ActionInfo reads are issued
-// together; the request chain itself is branch-free.  On return `ai` is the
-// ActionInfo of f.act.
-__device__ __forceinline__ void update_action_request(Fighter& f, const InputEval& e, AInfo& ai) {
+// RequestAction (F:472-510) as bit tests.  For the fighter's current (action, frame) the
+// 17-bit masks `take` / `buffer` hold the actions a request would switch to (the action has
+// ended; or it is alwaysCancelable and the request is another action) / would leave in
+// bufferActionID (inside the cancel window, listed in its mask, not itself).  A request
+// that switches replaces them by the new action's frame-0 masks (ReqInfo, fs_tables.h).
+struct ReqMasks {
+  uint32_t take, buffer;
+};
+
+__device__ __forceinline__ ReqMasks req_masks(const Fighter& f, AInfo ai) {
+  constexpr uint32_t kAll = (1u << kNumActions) - 1u;
+  const uint32_t self = 1u << f.act;
+  const bool ended = f.frame >= ai_frame_count(ai);
+  const bool ac = ai_always_cancel(ai);
+  const bool inwin = (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai));
+  ReqMasks m;
+  m.take = ended ? kAll : (ac ? (kAll & ~self) : 0u);
+  m.buffer = (!ended & !ac & inwin) ? (ai_cancel_mask(ai) & ~self) : 0u;
+  return m;
+}
+
+typedef uint32_t RInfo __attribute__((ext_vector_type(4)));  // ReqInfo: take0, buffer0, rec0, pad
+__device__ __forceinline__ RInfo req_info(int a) { return reinterpret_cast<const RInfo*>(sT.req)[a]; }
+
+// One RequestAction(a) of a chain; `took` / `rec` collect what SetCurrentAction did.
+__device__ __forceinline__ void request(Fighter& f, ReqMasks& m, bool& took, uint32_t& rec, int a, RInfo q,
+                                        bool valid) {
+  const bool take = valid & (((m.take >> a) & 1u) != 0);
+  const bool buffer = valid & !take & (((m.buffer >> a) & 1u) != 0);
+  f.act = take ? a : f.act;
+  f.buf = take ? NONE : (buffer ? a : f.buf);
+  m.take = take ? q.x : m.take;
+  m.buffer = take ? q.y : m.buffer;
+  rec = take ? q.z : rec;
+  took |= take;
+}
+
+// UpdateActionRequest (F:201-286).  Every request target is decided from the inputs and the
+// state before the first request, so the four ReqInfo reads are issued together; the chain
+// is branch-free.  Returns whether SetCurrentAction ran; then *rec is the new action's
+// frame-0 record.
+__device__ __forceinline__ bool update_action_request(Fighter& f, const InputEval& e, AInfo ai, uint32_t* rec) {
+  ReqMasks m = req_masks(f, ai);
+  bool took = false;
+  uint32_t r = 0;
   if (f.won) {  // F:204-208 (hasWon is only set between KO and the next SetupBattleStart)
-    request_action(f, ai, A_WIN, action_info(A_WIN), true);
-    return;
+    request(f, m, took, r, A_WIN, req_info(A_WIN), true);
+    f.frame = took ? 0 : f.frame;
+    f.hits = took ? 0 : f.hits;
+    f.rsv = took ? NONE : f.rsv;
+    *rec = r;
+    return took;
   }
   // reserved damage action, then buffered cancel: SetCurrentAction and return (F:212-229)
   const int rsv = f.rsv, buf = f.buf;
@@ -374,21 +397,23 @@ __device__ __forceinline__ void update_action_request(Fighter& f, const InputEva
                  : e.fwd          ? A_FORWARD
                  : e.back         ? (f.prox ? A_GUARD_PROXIMITY : A_BACKWARD)
                                   : A_STAND;
-  AInfo i0 = action_info(early ? a0 : 0), i1 = action_info(a1), i2 = action_info(a2), i3 = action_info(a3);
+  RInfo q0 = req_info(early ? a0 : 0), q1 = req_info(a1), q2 = req_info(a2), q3 = req_info(a3);
   // materialise all four here: left alone, the compiler sinks a read into the branch it
   // makes of a request's `take`, a second dependent LDS round trip
-  asm volatile("" : "+v"(i0), "+v"(i1), "+v"(i2), "+v"(i3));
+  asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+  request(f, m, took, r, a1, q1, !early & (e.special | e.atk_down));
+  request(f, m, took, r, a2, q2, !early & (e.fdash | e.bdash));
+  request(f, m, took, r, a3, q3, !early);
+  const bool set = took | early;  // SetCurrentAction ran (F:546-563)
   f.act = early ? a0 : f.act;
-  ai = early ? i0 : ai;
-  f.frame = early ? 0 : f.frame;
-  f.hits = early ? 0 : f.hits;
+  f.frame = set ? 0 : f.frame;
+  f.hits = set ? 0 : f.hits;
+  f.rsv = set ? NONE : f.rsv;
   f.buf = early ? NONE : f.buf;
-  f.rsv = early ? NONE : f.rsv;
-  request_action(f, ai, a1, i1, !early & (e.special | e.atk_down));
-  request_action(f, ai, a2, i2, !early & (e.fdash | e.bdash));
-  request_action(f, ai, a3, i3, !early);
   f.in_back = early ? f.in_back : e.back;  // for proximity guard (F:263)
   f.prox = early ? f.prox : false;         // F:285
+  *rec = early ? q0.z : r;
+  return set;
 }
 
 // UpdateMovement (F:291-319).  FORWARD / BACKWARD walk at the fighter speeds; any
@@ -447,8 +472,11 @@ __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
 
 // BoxBase.Overlaps (F:17-25), inclusive; `self` is the hitbox, `other` the hurtbox.
 // Boxes are (world x, width/2, yMin, yMax): xMin = x - w/2, xMax = x + w/2 (F:12-13).
+typedef float Box4 __attribute__((ext_vector_type(4)));  // (x offset, width/2, yMin, yMax) in registers
+__device__ __forceinline__ Box4 box4(const float4& b) { return *reinterpret_cast<const Box4*>(&b); }
+
 template <int FM>
-__device__ __forceinline__ bool box_overlaps(float sx, float4 sr, float ox, float4 orr) {
+__device__ __forceinline__ bool box_overlaps(float sx, Box4 sr, float ox, Box4 orr) {
   const bool c1 = fadd<FM>(ox, orr.y) >= fsub<FM>(sx, sr.y);
   const bool c2 = fsub<FM>(ox, orr.y) <= fadd<FM>(sx, sr.y);
   const bool c3 = orr.w >= sr.z;
@@ -502,8 +530,8 @@ struct BoxHits {
 };
 
 template <int FM>
-__device__ __forceinline__ BoxHits box_hits(uint32_t att_info, float4 h0, float4 h1, float hx0, float hx1,
-                                            uint32_t def_info, float4 u0, float4 u1, float ux0, float ux1) {
+__device__ __forceinline__ BoxHits box_hits(uint32_t att_info, Box4 h0, Box4 h1, float hx0, float hx1,
+                                            uint32_t def_info, Box4 u0, Box4 u1, float ux0, float ux1) {
   const int nh = (att_info >> 2) & 3, nu = def_info & 3;
   const bool v0 = nu > 0, v1 = nu > 1;
   BoxHits r;
@@ -780,17 +808,17 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
 // B's -- and phase B is resolved for both possible P2 hit counts, so only the
 // outcomes cross the pair: A's result to P1 (NotifyAttackHit), whether P2 was hit to
 // P1 (to pick B's variant), B's result to P2, and each defender's stun to the other.
+// The record boxes (my hurtboxes, the partner's hitboxes) are read from LDS together with
+// the frame record (one round trip) rather than here.
 template <int FM>
-__device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k) {
+__device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, Box4 my_hurt0, Box4 my_hurt1,
+                                                         Box4 their_hit0, Box4 their_hit1) {
   const uint32_t o_info = xpair(f.info);
   if ((((f.info | o_info) >> 2) & 3) == 0) return;  // only attack actions carry hitboxes
-  const int o_rec = xpair(f.rec);
   const int o_hits = xpair(f.hits);
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
-  const FrameRec& mine = sT.recs[f.rec];
-  const FrameRec& theirs = sT.recs[o_rec];
-  const BoxHits bh = box_hits<FM>(o_info, theirs.hit[0], theirs.hit[1], o_hx0, o_hx1, f.info, mine.hurt[0],
-                                  mine.hurt[1], f.ux0, f.ux1);
+  const BoxHits bh = box_hits<FM>(o_info, their_hit0, their_hit1, o_hx0, o_hx1, f.info, my_hurt0, my_hurt1,
+                                  f.ux0, f.ux1);
   // phase A on the P2 lane: P1 attacks P2
   HitTest tA = resolve(bh, o_hits);
   int stunA = 0;
@@ -905,7 +933,7 @@ __device__ __forceinline__ void write_obs(const Lane& L, uint8_t* guard, uint8_t
   position[c] = L.f.x;
   action[c] = L.rec_count > 0 ? (uint8_t)L.rec : 0;
   hitstun[c] = (uint8_t)L.f.stun;
-  if (L.k == 0) frame[r] = L.frame_count;
+  frame[r] = L.frame_count;  // both lanes hold the replica: the same value to the same address
 }
 
 __device__ __forceinline__ void write_main(const Lane& L, const DevOutputs& o, uint32_t r) {
@@ -950,11 +978,9 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.ai = action_info(L.f.act);
     settle(next);
     write_main(L, o, r);
-    if (k == 0) {
-      o.reward[r] = 0.0;
-      o.terminated[r] = 0;
-      o.truncated[r] = 0;
-    }
+    o.reward[r] = 0.0;  // per-arena outputs: both lanes store the same value (no divergent branch)
+    o.terminated[r] = 0;
+    o.truncated[r] = 0;
     return;
   }
   // the actor inputs of this frame (TrainingManager.p1Input/p2Input, BC:383-447)
@@ -968,19 +994,27 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   }
   const float sign = k == 0 ? 1.0f : -1.0f;
   const InputEval e = update_input(L.f, L.act, (int)k);
-  AInfo ai = L.ai;  // ActionInfo of f.act, carried from the previous tick
+  const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
   increment_action_frame(L.f, ai);
-  // the record if the action continues, read alongside the request's ActionInfo reads;
-  // a request that changes (or restarts) the action sets frame 0, whose record is ai.rec0
+  // the record if the action continues, read alongside the request's ReqInfo reads; a
+  // request that sets an action returns that action's frame-0 record
   const int rec_cont = frame_record(L.f);
-  update_action_request(L.f, e, ai);
-  L.f.rec = L.f.frame == 0 ? ai_rec0(ai) : rec_cont;
+  uint32_t rec_set;
+  const bool set = update_action_request(L.f, e, ai, &rec_set);
+  L.f.rec = set ? (int)rec_set : rec_cont;
   const FrameRec& R = sT.recs[L.f.rec];
+  // the collision's boxes: mine and the partner's (its record index crosses the pair now)
+  const int o_rec = xpair(L.f.rec);
+  const Box4 my_hurt0 = box4(R.hurt[0]), my_hurt1 = box4(R.hurt[1]);
+  const Box4 their_hit0 = box4(sT.recs[o_rec].hit[0]), their_hit1 = box4(sT.recs[o_rec].hit[1]);
   update_movement<FM>(L.f, sign, R.vel);
   update_boxes<FM>(L.f, sign, R);
   push_character_vs_character<FM>(L.f, k);
   push_character_vs_background<FM>(L.f);
-  hitbox_hurtbox_collision<FM>(L.f, k);
+  // consumed here, unconditionally, so the reads stay where they were issued (next to the
+  // frame record) instead of being sunk into the collision's branch
+  asm volatile("" ::"v"(my_hurt0), "v"(my_hurt1), "v"(their_hit0), "v"(their_hit1));
+  hitbox_hurtbox_collision<FM>(L.f, k, my_hurt0, my_hurt1, their_hit0, their_hit1);
   // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes
   const uint32_t mine = (uint32_t)L.f.vital | ((uint32_t)L.f.guard << 2) | ((uint32_t)guard_before << 4);
   const uint32_t theirs = xpair(mine);
@@ -1018,13 +1052,11 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     }
     L.has_term = false;
   }
-  L.ai = action_info(L.f.act);  // hits and resets set actions too; its latency hides behind the stores
+  L.ai = action_info(L.f.act);  // for the next tick (hits and resets set actions too)
   write_main(L, o, r);
-  if (k == 0) {
-    o.reward[r] = reward;
-    o.terminated[r] = over ? 1 : 0;
-    o.truncated[r] = 0;
-  }
+  o.reward[r] = reward;  // identical on both lanes of the arena
+  o.terminated[r] = over ? 1 : 0;
+  o.truncated[r] = 0;
 }
 
 // One launch over all arenas, `TICKS` = 1 (k_step, the per-step VectorEnv path) or

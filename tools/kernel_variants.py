@@ -27,27 +27,53 @@ def _edit_fn(src, signature_start, body_prefix):
     return src[:j + 1] + "\n" + body_prefix + src[j + 1:]
 
 
+ENV_STEP = "__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own"
+VNOP100 = "  asm volatile(\"" + "v_nop\\n" * 100 + "\");"
+LDS2 = ("  { uint32_t d0; asm volatile(\"ds_read_b32 %0, %1\\n s_waitcnt lgkmcnt(0)\\n v_and_b32 %0, 0xfc, %0\\n "
+        "ds_read_b32 %0, %0\\n s_waitcnt lgkmcnt(0)\" : \"=v\"(d0) : \"v\"((uint32_t)0)); (void)d0; }")
+SALU50 = "  { uint32_t s0 = 0; asm volatile(\"" + "s_add_u32 %0, %0, 1\\n" * 50 + "\" : \"+s\"(s0)); }"
+
+VADD100_IND = ("  { uint32_t r0 = 1, r1 = 2, r2 = 3, r3 = 4; asm volatile(\"" +
+               "v_add_u32 %0, 1, %0\\n v_add_u32 %1, 1, %1\\n v_add_u32 %2, 1, %2\\n v_add_u32 %3, 1, %3\\n" * 25 +
+               "\" : \"+v\"(r0), \"+v\"(r1), \"+v\"(r2), \"+v\"(r3)); }")
+VADD100_DEP = "  { uint32_t r0 = 1; asm volatile(\"" + "v_add_u32 %0, 1, %0\\n" * 100 + "\" : \"+v\"(r0)); }"
+VOP3_100 = ("  { uint32_t r0 = 1, r1 = 2, r2 = 3, r3 = 4; asm volatile(\"" +
+            "v_add3_u32 %0, %0, 1, %1\\n v_add3_u32 %1, %1, 1, %2\\n v_add3_u32 %2, %2, 1, %3\\n "
+            "v_add3_u32 %3, %3, 1, %0\\n" * 25 + "\" : \"+v\"(r0), \"+v\"(r1), \"+v\"(r2), \"+v\"(r3)); }")
+
 VARIANTS = {
     "base": lambda s: s,
+    "plus_100_vadd_ind": lambda s: _edit_fn(s, ENV_STEP, VADD100_IND),
+    "plus_100_vadd_dep": lambda s: _edit_fn(s, ENV_STEP, VADD100_DEP),
+    "plus_100_vop3": lambda s: _edit_fn(s, ENV_STEP, VOP3_100),
+    "plus_100_valu": lambda s: _edit_fn(s, ENV_STEP, VNOP100),
+    "plus_2_lds_rt": lambda s: _edit_fn(s, ENV_STEP, LDS2),
+    "plus_50_salu": lambda s: _edit_fn(s, ENV_STEP, SALU50),
     "no_stores": lambda s: _edit_fn(_edit_fn(s, "__device__ __forceinline__ void write_obs(", "  return;"),
                                     "__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own",
                                     "  const_cast<StepParams&>(p).dense_reward = p.dense_reward;"
                                     ).replace("    o.reward[r] = reward;\n", "").replace(
                                         "    o.terminated[r] = over ? 1 : 0;\n", "").replace(
                                         "    o.truncated[r] = 0;\n", ""),
-    "const_actions": lambda s: s.replace(
+    "_const_actions": lambda s: s.replace(
         "    else return src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a];",
         "    else return (uint32_t)(t * 5 + a) & 7u;"),
-    "no_collision": lambda s: _edit_fn(s, "__device__ __forceinline__ void hitbox_hurtbox_collision(", "  return;"),
-    "no_push": lambda s: _edit_fn(s, "__device__ __forceinline__ void push_character_vs_character(", "  return;"),
-    "no_request": lambda s: _edit_fn(s, "__device__ __forceinline__ void update_action_request(", "  return;"),
+    "_no_collision": lambda s: _edit_fn(s, "__device__ __forceinline__ void hitbox_hurtbox_collision(", "  return;"),
+    "_no_push": lambda s: _edit_fn(s, "__device__ __forceinline__ void push_character_vs_character(", "  return;"),
+    "_no_request": lambda s: _edit_fn(s, "__device__ __forceinline__ void update_action_request(", "  return;"),
 }
+
+
+def active():
+    """Variants whose name starts with "_" change the game's dynamics (removed phases alter
+    what the arenas do), so their times are not comparable; they are kept but not run."""
+    return {k: v for k, v in VARIANTS.items() if not k.startswith("_")}
 
 
 def build():
     sys.path.insert(0, ROOT)
     from footsies_gym_amd import build as B
-    for name, fn in VARIANTS.items():
+    for name, fn in active().items():
         d = os.path.join(EXP, name)
         os.makedirs(d, exist_ok=True)
         for f in os.listdir(CSRC):
@@ -101,7 +127,7 @@ print("%%.1f" %% d[len(d) // 2])
 
 
 def time_all(N=65536, T=2000):
-    for name in VARIANTS:
+    for name in active():
         print("%-14s median us per 100-tick launch: %s" % (name, time_one(os.path.join(EXP, name, "libfootsies.so"),
                                                                           N, T)), flush=True)
 
