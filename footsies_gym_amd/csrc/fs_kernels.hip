@@ -193,26 +193,6 @@ __device__ __forceinline__ float fsub(float a, float b) {
   if constexpr (FM == FS_FLOAT_DOUBLE) return (float)__dsub_rn((double)a, (double)b);
   else return __fsub_rn(a, b);
 }
-// basePosition.x + (dataRect.x * sign)   (TransformToFightRect, F:706-719)
-template <int FM>
-__device__ __forceinline__ float xform(float base, float rx, float sign) {
-  if constexpr (FM == FS_FLOAT_DOUBLE) return (float)__dadd_rn((double)base, __dmul_rn((double)rx, (double)sign));
-  else return __fadd_rn(base, __fmul_rn(rx, sign));
-}
-// position.x += v * sign * Time.deltaTime   (F:300, 316)
-template <int FM>
-__device__ __forceinline__ float pos_plus_vel(float pos, float v, float sign) {
-  if constexpr (FM == FS_FLOAT_DOUBLE)
-    return (float)__dadd_rn((double)pos, __dmul_rn(__dmul_rn((double)v, (double)sign), (double)kDt));
-  else return __fadd_rn(pos, __fmul_rn(__fmul_rn(v, sign), kDt));
-}
-// position.x -= v * sign * Time.deltaTime   (F:305)
-template <int FM>
-__device__ __forceinline__ float pos_minus_vel(float pos, float v, float sign) {
-  if constexpr (FM == FS_FLOAT_DOUBLE)
-    return (float)__dsub_rn((double)pos, __dmul_rn(__dmul_rn((double)v, (double)sign), (double)kDt));
-  else return __fsub_rn(pos, __fmul_rn(__fmul_rn(v, sign), kDt));
-}
 // BoxBase.xMin / xMax (F:12-13): x is the centre
 template <int FM>
 __device__ __forceinline__ float bb_xmin(float x, float w) {
@@ -419,11 +399,15 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
 // UpdateMovement (F:291-319).  FORWARD / BACKWARD walk at the fighter speeds; any
 // other action takes the first movement window's velocity (0 = none).  BACKWARD's
 // `pos -= s*sign*dt` is `pos + (-s)*sign*dt` bit for bit (negation is exact and
-// round-to-nearest is symmetric), so one expression covers all three.
+// round-to-nearest is symmetric), so one expression covers all three; `v*sign` is exact
+// too, so the velocities arrive pre-signed (walk speeds per lane, the facing-left frame
+// records negated) and the step is pos + v*dt.
 template <int FM>
-__device__ __forceinline__ void update_movement(Fighter& f, float sign, float rec_vel) {
-  const float v = f.act == A_FORWARD ? kForwardSpeed : f.act == A_BACKWARD ? -kBackwardSpeed : rec_vel;
-  const float nx = pos_plus_vel<FM>(f.x, v, sign);
+__device__ __forceinline__ void update_movement(Fighter& f, float walk_fwd, float walk_back, float rec_vel) {
+  const float v = f.act == A_FORWARD ? walk_fwd : f.act == A_BACKWARD ? walk_back : rec_vel;
+  float nx;
+  if constexpr (FM == FS_FLOAT_DOUBLE) nx = (float)__dadd_rn((double)f.x, __dmul_rn((double)v, (double)kDt));
+  else nx = __fadd_rn(f.x, __fmul_rn(v, kDt));
   f.x = (f.stun <= 0 && v != 0.0f) ? nx : f.x;
 }
 
@@ -432,18 +416,19 @@ __device__ __forceinline__ int frame_record(const Fighter& f) {
   return sT.rec_index[f.act * kFrameStride + min(f.frame, kFrameStride - 1)];
 }
 
-// UpdateBoxes (F:671-697): world x of every box of the record
+// UpdateBoxes (F:671-697): world x of every box of the record, `R` being the record in
+// the fighter's facing (x offsets pre-signed): basePosition.x + dataRect.x * sign.
 template <int FM>
-__device__ __forceinline__ void update_boxes(Fighter& f, float sign, const FrameRec& R) {
+__device__ __forceinline__ void update_boxes(Fighter& f, const FrameRec& R) {
   f.info = R.info;
   f.pw = R.push.y;
   f.pymin = R.push.z;
   f.pymax = R.push.w;
-  f.px = xform<FM>(f.x, R.push.x, sign);
-  f.ux0 = xform<FM>(f.x, R.hurt[0].x, sign);
-  f.ux1 = xform<FM>(f.x, R.hurt[1].x, sign);
-  f.hx0 = xform<FM>(f.x, R.hit[0].x, sign);
-  f.hx1 = xform<FM>(f.x, R.hit[1].x, sign);
+  f.px = fadd<FM>(f.x, R.push.x);
+  f.ux0 = fadd<FM>(f.x, R.hurt[0].x);
+  f.ux1 = fadd<FM>(f.x, R.hurt[1].x);
+  f.hx0 = fadd<FM>(f.x, R.hit[0].x);
+  f.hx1 = fadd<FM>(f.x, R.hit[1].x);
 }
 
 // ApplyPositionChange (F:331-350): position and every box are shifted, not rebuilt
@@ -470,19 +455,10 @@ __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
   }
 }
 
-// BoxBase.Overlaps (F:17-25), inclusive; `self` is the hitbox, `other` the hurtbox.
-// Boxes are (world x, width/2, yMin, yMax): xMin = x - w/2, xMax = x + w/2 (F:12-13).
+// BoxBase (F:8-26): boxes are (world x, width/2, yMin, yMax); xMin = x - w/2, xMax = x + w/2
+// (F:12-13) and Overlaps is inclusive.  The hit test below evaluates it per box pair.
 typedef float Box4 __attribute__((ext_vector_type(4)));  // (x offset, width/2, yMin, yMax) in registers
 __device__ __forceinline__ Box4 box4(const float4& b) { return *reinterpret_cast<const Box4*>(&b); }
-
-template <int FM>
-__device__ __forceinline__ bool box_overlaps(float sx, Box4 sr, float ox, Box4 orr) {
-  const bool c1 = fadd<FM>(ox, orr.y) >= fsub<FM>(sx, sr.y);
-  const bool c2 = fsub<FM>(ox, orr.y) <= fadd<FM>(sx, sr.y);
-  const bool c3 = orr.w >= sr.z;
-  const bool c4 = orr.z <= sr.w;
-  return c1 & c2 & c3 & c4;
-}
 
 constexpr int DR_DAMAGE = 1, DR_GUARD = 2, DR_GUARD_BREAK = 3;
 
@@ -534,11 +510,19 @@ __device__ __forceinline__ BoxHits box_hits(uint32_t att_info, Box4 h0, Box4 h1,
                                             uint32_t def_info, Box4 u0, Box4 u1, float ux0, float ux1) {
   const int nh = (att_info >> 2) & 3, nu = def_info & 3;
   const bool v0 = nu > 0, v1 = nu > 1;
+  // BoxBase.Overlaps (F:17-25) per pair, with each box's xMin / xMax computed once
+  const float h0min = fsub<FM>(hx0, h0.y), h0max = fadd<FM>(hx0, h0.y);
+  const float h1min = fsub<FM>(hx1, h1.y), h1max = fadd<FM>(hx1, h1.y);
+  const float u0min = fsub<FM>(ux0, u0.y), u0max = fadd<FM>(ux0, u0.y);
+  const float u1min = fsub<FM>(ux1, u1.y), u1max = fadd<FM>(ux1, u1.y);
+  auto ov = [](float smin, float smax, Box4 s, float omin, float omax, Box4 o) {
+    return (omax >= smin) & (omin <= smax) & (o.w >= s.z) & (o.z <= s.w);
+  };
   BoxHits r;
   r.b0 = (att_info >> 4) & 31;
   r.b1 = (att_info >> 9) & 31;
-  r.any0 = (nh > 0) & ((v0 & box_overlaps<FM>(hx0, h0, ux0, u0)) | (v1 & box_overlaps<FM>(hx0, h0, ux1, u1)));
-  r.any1 = (nh > 1) & ((v0 & box_overlaps<FM>(hx1, h1, ux0, u0)) | (v1 & box_overlaps<FM>(hx1, h1, ux1, u1)));
+  r.any0 = (nh > 0) & ((v0 & ov(h0min, h0max, h0, u0min, u0max, u0)) | (v1 & ov(h0min, h0max, h0, u1min, u1max, u1)));
+  r.any1 = (nh > 1) & ((v0 & ov(h1min, h1max, h1, u0min, u0max, u0)) | (v1 & ov(h1min, h1max, h1, u1min, u1max, u1)));
   return r;
 }
 
@@ -773,31 +757,31 @@ __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int
 }
 
 // UpdatePushCharacterVsCharacter (BC:483-501) with UnityEngine.Rect semantics:
-// x is xMin, xMax = width + x, Overlaps is strict.  Both lanes evaluate the same
-// expressions on (P1, P2) values; each applies its own fighter's shift.
+// x is xMin, xMax = width + x, Overlaps is strict; each lane applies its own fighter's
+// shift.  The y-test is dropped when tools/gen_tables.py proves every pair of pushboxes
+// overlaps vertically (kPushYAlwaysOverlaps).
 template <int FM>
 __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t k) {
-  const float o_px = xpair(f.px), o_x = xpair(f.x);
-  const float o_pw = xpair(f.pw), o_pymin = xpair(f.pymin), o_pymax = xpair(f.pymax);
-  const float px1 = k == 0 ? f.px : o_px, px2 = k == 0 ? o_px : f.px;
-  const float x1 = k == 0 ? f.x : o_x, x2 = k == 0 ? o_x : f.x;
-  // record pushboxes are (x offset, width, yMin, yMax); position.y == 0
-  const float4 mine = make_float4(0.0f, f.pw, f.pymin, f.pymax), theirs = make_float4(0.0f, o_pw, o_pymin, o_pymax);
-  const float4 r1 = k == 0 ? mine : theirs, r2 = k == 0 ? theirs : mine;
-  const float xmax1 = fadd<FM>(r1.y, px1), xmax2 = fadd<FM>(r2.y, px2);
-  const bool overlap = (xmax2 > px1) & (px2 < xmax1) & (r2.w > r1.z) & (r2.z < r1.w);
-  if (!overlap || x1 == x2) return;  // a tie pushes nothing (BC:490-499)
-  float d1, d2;  // shifts of P1, P2
-  if constexpr (FM == FS_FLOAT_DOUBLE) {
-    const double d = x1 < x2 ? (double)xmax1 - (double)px2 : (double)xmax2 - (double)px1;
-    d1 = x1 < x2 ? (float)(d * -1 / 2) : (float)(d * 1 / 2);
-    d2 = x1 < x2 ? (float)(d * 1 / 2) : (float)(d * -1 / 2);
-  } else {
-    const float d = x1 < x2 ? __fsub_rn(xmax1, px2) : __fsub_rn(xmax2, px1);
-    d1 = x1 < x2 ? d * -1.0f / 2.0f : d * 1.0f / 2.0f;
-    d2 = x1 < x2 ? d * 1.0f / 2.0f : d * -1.0f / 2.0f;
+  // The test and the shift are symmetric in the two fighters, so each lane evaluates them
+  // as (mine, partner's) -- the same operations on the same values as (P1, P2).
+  const float o_px = xpair(f.px), o_x = xpair(f.x), o_pw = xpair(f.pw);
+  const float xmax_m = fadd<FM>(f.pw, f.px), xmax_o = fadd<FM>(o_pw, o_px);  // Rect.xMax = width + x
+  bool overlap = (xmax_o > f.px) & (o_px < xmax_m);
+  if constexpr (!kPushYAlwaysOverlaps) {  // record pushboxes are (x offset, width, yMin, yMax)
+    const float o_ymin = xpair(f.pymin), o_ymax = xpair(f.pymax);
+    overlap = overlap & (o_ymax > f.pymin) & (o_ymin < f.pymax);
   }
-  apply_position_change<FM>(f, k == 0 ? d1 : d2);
+  if (!overlap || f.x == o_x) return;  // a tie pushes nothing (BC:490-499)
+  const bool left = f.x < o_x;         // the left fighter moves by -d/2, the right one by +d/2
+  float dx;
+  if constexpr (FM == FS_FLOAT_DOUBLE) {
+    const double d = left ? (double)xmax_m - (double)o_px : (double)xmax_o - (double)f.px;
+    dx = left ? (float)(d * -1 / 2) : (float)(d * 1 / 2);
+  } else {
+    const float d = left ? __fsub_rn(xmax_m, o_px) : __fsub_rn(xmax_o, f.px);
+    dx = left ? d * -1.0f / 2.0f : d * 1.0f / 2.0f;
+  }
+  apply_position_change<FM>(f, dx);
 }
 
 // UpdateHitboxHurtboxCollision (BC:521-591): attacker P1 (phase A), then attacker P2
@@ -992,7 +976,8 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.rec = L.act;
     L.rec_count++;
   }
-  const float sign = k == 0 ? 1.0f : -1.0f;
+  const float walk_fwd = k == 0 ? kForwardSpeed : -kForwardSpeed;    // speed * sign
+  const float walk_back = k == 0 ? -kBackwardSpeed : kBackwardSpeed;  // -speed * sign
   const InputEval e = update_input(L.f, L.act, (int)k);
   const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
   increment_action_frame(L.f, ai);
@@ -1002,13 +987,13 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   uint32_t rec_set;
   const bool set = update_action_request(L.f, e, ai, &rec_set);
   L.f.rec = set ? (int)rec_set : rec_cont;
-  const FrameRec& R = sT.recs[L.f.rec];
+  const FrameRec& R = sT.recs[k][L.f.rec];
   // the collision's boxes: mine and the partner's (its record index crosses the pair now)
   const int o_rec = xpair(L.f.rec);
   const Box4 my_hurt0 = box4(R.hurt[0]), my_hurt1 = box4(R.hurt[1]);
-  const Box4 their_hit0 = box4(sT.recs[o_rec].hit[0]), their_hit1 = box4(sT.recs[o_rec].hit[1]);
-  update_movement<FM>(L.f, sign, R.vel);
-  update_boxes<FM>(L.f, sign, R);
+  const Box4 their_hit0 = box4(sT.recs[0][o_rec].hit[0]), their_hit1 = box4(sT.recs[0][o_rec].hit[1]);
+  update_movement<FM>(L.f, walk_fwd, walk_back, R.vel);
+  update_boxes<FM>(L.f, R);
   push_character_vs_character<FM>(L.f, k);
   push_character_vs_background<FM>(L.f);
   // consumed here, unconditionally, so the reads stay where they were issued (next to the
@@ -1021,13 +1006,17 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   const uint32_t w1 = k == 0 ? mine : theirs, w2 = k == 0 ? theirs : mine;
   const int v1 = w1 & 3, v2 = w2 & 3;
   const bool over = v1 <= 0 || v2 <= 0;
-  double reward;
+  double reward = 0.0;
   if (p.dense_reward) {
-    reward = 0.0;
-    if (((w1 >> 2) & 3) < (w1 >> 4)) reward -= 0.3;
-    if (((w2 >> 2) & 3) < (w2 >> 4)) reward += 0.3;
-    L.cum += reward;
-    if (over) reward += (double)(v2 == 0 ? 1 : -1) - L.cum;
+    // Only a guard drop or the round's end moves the f64 sums: on other ticks the reward is
+    // 0.0 and `cum += 0.0` is exact (cum starts at +0.0 and a sum of nonzero terms is never -0.0).
+    const bool g1 = ((w1 >> 2) & 3) < (w1 >> 4), g2 = ((w2 >> 2) & 3) < (w2 >> 4);
+    if (g1 | g2 | over) {
+      if (g1) reward -= 0.3;
+      if (g2) reward += 0.3;
+      L.cum += reward;
+      if (over) reward += (double)(v2 == 0 ? 1 : -1) - L.cum;
+    }
   } else {
     reward = over ? (v2 == 0 ? 1.0 : -1.0) : 0.0;
   }
