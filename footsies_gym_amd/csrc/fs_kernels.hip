@@ -803,31 +803,32 @@ __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k,
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
   const BoxHits bh = box_hits<FM>(o_info, their_hit0, their_hit1, o_hx0, o_hx1, f.info, my_hurt0, my_hurt1,
                                   f.ux0, f.ux1);
-  // phase A on the P2 lane: P1 attacks P2
-  HitTest tA = resolve(bh, o_hits);
-  int stunA = 0;
-  if (k == 1 && tA.hit) {
-    const AttackInfo ad = sT.attacks[tA.atk];
-    const int res = notify_damaged(f, ad);
-    stunA = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
-  }
-  if (k == 1 && !tA.hit && tA.prox && f.in_back) f.prox = true;  // NotifyInProximityGuardRange (F:400-406)
-  const uint32_t a_bits = xpair((uint32_t)tA.hit | ((uint32_t)stunA << 1));
-  const bool hitA = k == 1 ? tA.hit : (a_bits & 1);
-  stunA = k == 1 ? stunA : (int)(a_bits >> 1);
+  // phase A (P1 attacks P2) is resolved on the P2 lane; its outcome crosses to P1, whose lane
+  // then resolves phase B (P2 attacks P1) with P2's hit count after phase A
+  const HitTest tA = resolve(bh, o_hits);
+  // (every exchange is its own statement on both lanes: inside a select the compiler may run
+  // the DPP move under a one-lane exec mask, and a disabled source lane reads as 0)
+  const uint32_t partner_hitA = xpair((uint32_t)tA.hit);
+  const bool hitA = k == 1 ? tA.hit : (partner_hitA & 1u) != 0;
+  const HitTest tB = resolve(bh, hitA ? 0 : o_hits);
+  // each lane is the defender of exactly one phase: one NotifyDamaged per lane.  Order per
+  // fighter as in the reference: P1 gets NotifyAttackHit (A) before its NotifyDamaged (B);
+  // P2 its NotifyDamaged (A) before NotifyAttackHit (B).
+  const bool my_hit = k == 1 ? tA.hit : tB.hit;
+  const int my_atk = k == 1 ? tA.atk : tB.atk;
+  const bool my_prox = k == 1 ? tA.prox : tB.prox;
   if (k == 0 && hitA) f.hits++;  // NotifyAttackHit for P1 (F:352-355)
-  // phase B on the P1 lane: P2 attacks P1 with its hit count after phase A
-  HitTest tB = resolve(bh, hitA ? 0 : o_hits);
-  int stunB = 0;
-  if (k == 0 && tB.hit) {
-    const AttackInfo ad = sT.attacks[tB.atk];
+  int my_stun = 0;
+  if (my_hit) {
+    const AttackInfo ad = sT.attacks[my_atk];
     const int res = notify_damaged(f, ad);
-    stunB = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
+    my_stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
   }
-  if (k == 0 && !tB.hit && tB.prox && f.in_back) f.prox = true;
-  const uint32_t b_bits = xpair((uint32_t)tB.hit | ((uint32_t)stunB << 1));
-  const bool hitB = k == 0 ? tB.hit : (b_bits & 1);
-  stunB = k == 0 ? stunB : (int)(b_bits >> 1);
+  if (!my_hit && my_prox && f.in_back) f.prox = true;  // NotifyInProximityGuardRange (F:400-406)
+  const uint32_t other = xpair((uint32_t)my_hit | ((uint32_t)my_stun << 1));  // the partner's outcome
+  const bool hitB = k == 0 ? my_hit : (other & 1u) != 0;
+  const int stunA = k == 1 ? my_stun : (int)(other >> 1);
+  const int stunB = k == 0 ? my_stun : (int)(other >> 1);
   if (k == 1 && hitB) f.hits++;  // NotifyAttackHit for P2
   f.stun = hitB ? stunB : (hitA ? stunA : f.stun);  // SetHitStun on both, phase B last (BC:576-578)
 }
