@@ -43,6 +43,8 @@ VOP3_100 = ("  { uint32_t r0 = 1, r1 = 2, r2 = 3, r3 = 4; asm volatile(\"" +
 
 VARIANTS = {
     "base": lambda s: s,
+    "block512": lambda s: s.replace("constexpr int kBlock = 256;", "constexpr int kBlock = 512;").replace(
+        "__launch_bounds__(256)", "__launch_bounds__(512)"),
     "plus_100_vadd_ind": lambda s: _edit_fn(s, ENV_STEP, VADD100_IND),
     "plus_100_vadd_dep": lambda s: _edit_fn(s, ENV_STEP, VADD100_DEP),
     "plus_100_vop3": lambda s: _edit_fn(s, ENV_STEP, VOP3_100),
