@@ -84,3 +84,26 @@ def test_lockstep_4096_bot_long(oracle_lib):
     """Config 2 shape: 4096 arenas, random P1 vs scripted bot P2, 10k steps."""
     sim, ora = make_pair(oracle_lib, 4096, "bot", seed=0)
     run_lockstep(sim, ora, 10000, np.random.default_rng(123), state_every=500, sticky=0.5)
+
+
+@pytest.mark.parametrize("n_envs,ticks,p2", [(65536, 500, "external"), (262144, 200, "bot"), (262144, 200, "external")])
+def test_full_size_fused_matches_oracle(oracle_lib, n_envs, ticks, p2):
+    """BASELINE sizes (C3: 65 536 arenas; C4: 262 144 = 8 x 32 768 on one GPU): the fused kernel
+    with in-kernel hashed actions, in chunks, against the oracle on the same hashed stream --
+    every arena's full state and the last step's outputs bit-exact."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    p2m = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT}[p2]
+    sim = FootsiesSim(n_envs, p2_mode=p2, seed=17)
+    ora = oracle_lib.Oracle(n_envs, p2_mode=p2m, base_seed=17)
+    done = 0
+    for chunk in (1, 99, ticks - 100):
+        sim.step_n(chunk, None, None, action_seed=0xC3C4)
+        ora.step_n_hashed(chunk, 0xC3C4)
+        done += chunk
+    torch.cuda.synchronize()
+    assert done == ticks
+    compare_states(ora.state(), sim.get_state())
+    compare_outputs(ora.outputs(), sim.outputs_numpy())
+    sim.close()
+    ora.close()
