@@ -122,6 +122,34 @@ def policy_loop_rate(torch, N, steps, device):
                       "sampling + log-prob, fs_step per step, P2 = bot, HIP graph replay" % N}
 
 
+def fused_policy_rate(torch, N, steps, device, ticks=100):
+    """Config C5 fused: the same actor evaluated inside the simulator kernel (bf16 MFMAs,
+    fs_step_n_policy), `ticks` policy-driven ticks per launch, P1's actions and log-probs
+    stored per tick ([ticks][N] each, what a PPO rollout keeps); P2 = bot.  Timed with HIP
+    events on torch's current stream, where FootsiesSim issues its launches."""
+    from footsies_gym_amd.rollout import FusedPolicyRollout, make_actor
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
+    ro = FusedPolicyRollout(sim, make_actor(device=torch.device("cuda", device)), seed=1)
+    acts = torch.empty((ticks, N), dtype=torch.uint8, device=torch.device("cuda", device))
+    logp = torch.empty((ticks, N), dtype=torch.float32, device=torch.device("cuda", device))
+    ro.rollout(ticks, acts, logp)
+    torch.cuda.synchronize(device)
+    reps = max(1, steps // ticks)
+    stream = torch.cuda.current_stream(device)  # FootsiesSim issues on torch's current stream
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record(stream)
+    for _ in range(reps):
+        ro.rollout(ticks, acts, logp)
+    t1.record(stream)
+    torch.cuda.synchronize(device)
+    dt = t0.elapsed_time(t1) / 1e3
+    sim.close()
+    return {"value": N * reps * ticks / dt, "ms_per_step": 1e3 * dt / (reps * ticks), "ticks_per_launch": ticks,
+            "config": "C5 fused: %d arenas, the same actor in bf16 MFMA inside the tick loop (fs_step_n_policy), "
+                      "inverse-CDF sampling + log-prob stored per tick, P2 = bot" % N}
+
+
 def pmc_traffic(kernel, envs, ticks):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/*_traffic.json, written by tools/summarize_profile.py from separate
@@ -288,6 +316,10 @@ def main():
             out["policy_loop"] = policy_loop_rate(torch, N, min(K, 1000), local)
         except Exception as e:  # reported, never fatal to the headline measurement
             out["policy_loop"] = {"error": "%s: %s" % (type(e).__name__, e)}
+        try:
+            out["policy_loop_fused"] = fused_policy_rate(torch, N, max(K * chunk // 10, 1000), local)
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            out["policy_loop_fused"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)
     if rank == 0:

@@ -82,6 +82,13 @@ OUTPUT_SPEC = {
 }
 
 
+class fs_policy(C.Structure):
+    _fields_ = [
+        ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p), ("w3", C.c_void_p),
+        ("b3", C.c_void_p), ("seed", C.c_uint64), ("actions_out", C.c_void_p), ("logp_out", C.c_void_p),
+    ]
+
+
 class fs_env_state(C.Structure):
     _fields_ = [
         ("p1Vital", C.c_int32), ("p2Vital", C.c_int32), ("p1Guard", C.c_int32), ("p2Guard", C.c_int32),
@@ -122,6 +129,7 @@ LIB_FUNCTIONS = {
     "fs_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_masked": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_n": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(fs_outputs)]),
+    "fs_step_n_policy": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(fs_policy), C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_hash_actions": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "fs_outputs_get": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_bind_outputs": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),

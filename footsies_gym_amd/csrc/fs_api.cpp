@@ -265,7 +265,8 @@ FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int
 }
 
 static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2, int flags, uint64_t seed,
-                       const fs_outputs* traj, const uint8_t* active = nullptr) {
+                       const fs_outputs* traj, const uint8_t* active = nullptr,
+                       const fs_policy* pol = nullptr) {
   int rc;
   if ((rc = use_device(h))) return rc;
   const size_t N = (size_t)h->n;
@@ -279,6 +280,8 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
   sp.autoreset_mode = h->cfg.autoreset_mode;
   sp.action_seed = seed;
   sp.t0 = h->steps;
+  if (pol) sp.pol = fsk::PolicyParams{pol->w1, pol->b1, pol->w2, pol->b2, pol->w3, pol->b3,
+                                      pol->actions_out, pol->logp_out, pol->seed};
   const bool ext = h->cfg.p2_mode == FS_P2_EXTERNAL;
   if (flags == FS_ACT_HOST && p1) {
     if (n != 1) return set_err(h, FS_E_INVALID, "host actions are only accepted for single steps");
@@ -361,6 +364,22 @@ FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p
   if ((p1_act == nullptr) != (p2_act == nullptr) && h->cfg.p2_mode == FS_P2_EXTERNAL)
     return set_err(h, FS_E_INVALID, "fs_step_n: give both action arrays or neither");
   return step_common(h, n, p1_act, p2_act, FS_ACT_DEVICE, action_seed, traj);
+}
+
+FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint8_t* p2_act,
+                            const fs_outputs* traj) {
+  if (!h) return FS_E_INVALID;
+  if (!pol || !pol->w1 || !pol->b1 || !pol->w2 || !pol->b2 || !pol->w3 || !pol->b3)
+    return set_err(h, FS_E_INVALID, "fs_step_n_policy: all six weight arrays required");
+  if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n_policy: n must be > 0");
+  if ((uint64_t)n * (uint64_t)h->n * 2u > 0x7fffffffull)
+    return set_err(h, FS_E_INVALID, "fs_step_n_policy: n * num_envs too large for one launch; split it");
+  if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
+    return set_err(h, FS_E_INVALID, "fs_step_n_policy: p2 actions required for FS_P2_EXTERNAL");
+  if (h->cfg.frame_delay > 0)
+    return set_err(h, FS_E_UNSUPPORTED, "fs_step_n_policy: the actor observes undelayed frames; frame_delay > 0 "
+                                        "is not supported");
+  return step_common(h, n, nullptr, p2_act, FS_ACT_DEVICE, 0, traj, nullptr, pol);
 }
 
 FS_API int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out) {

@@ -40,9 +40,18 @@ struct DevOutputs {
   uint8_t* final_hitstun;
 };
 
+// the in-kernel actor of fs_step_n_policy (fs_policy.h): fp32 weights in torch layouts
+struct PolicyParams {
+  const float *w1, *b1, *w2, *b2, *w3, *b3;  // [64][8] [64] [64][64] [64] [8][64] [8]
+  uint8_t* actions;  // [n][N] or null
+  float* logp;       // [n][N] or null
+  uint64_t seed;
+};
+
 struct StepParams {
   DevState st;
   DevOutputs out;
+  PolicyParams pol;
   const uint8_t* p1;   // [n][N] or null (hashed)
   const uint8_t* p2;   // [n][N] or null
   const uint8_t* active;  // [N] or null: single-tick launches skip arenas whose byte is 0

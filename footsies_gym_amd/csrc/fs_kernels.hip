@@ -29,6 +29,7 @@
 
 #include "fs_internal.h"
 #include "fs_tables.h"
+#include "fs_policy.h"
 
 #pragma clang fp contract(off)
 
@@ -1049,10 +1050,24 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   o.truncated[r] = 0;
 }
 
+// P1's observation features for the in-kernel actor (fs_policy.h), packed bf16x2:
+// guard / 3 | move / 16 and move_frame / 55 | position / 4.6, the values write_obs stores
+// (FE:339-358, 537-549) scaled by f32 reciprocals.
+__device__ __forceinline__ void policy_features(const Lane& L, uint32_t& d0, uint32_t& d1) {
+  int a = L.f.act;
+  if (a == A_DEAD || a == A_WIN) a = A_STAND;
+  const int mf = (a == A_STAND || a == A_FORWARD || a == A_BACKWARD) ? 0 : L.f.frame;
+  d0 = pack_bf16x2((float)L.f.guard * (1.0f / 3.0f), (float)a * (1.0f / 16.0f));
+  d1 = pack_bf16x2((float)mf * (1.0f / 55.0f), L.f.x * (1.0f / 4.6f));
+}
+
 // One launch over all arenas, `TICKS` = 1 (k_step, the per-step VectorEnv path) or
 // p.n_steps (k_step_n*, the fused rollout: state stays in registers between ticks).
 // HASH draws the actions in-kernel from splitmix64 instead of reading action rows.
-template <int FM, int P2, bool FUSED, bool HASH>
+// POL samples P1's action every tick from the MLP actor (fs_policy.h); its MFMAs and lane
+// exchanges need the whole wave, so lanes past the last arena stay in the loop (on a copy
+// of arena 0 that they never store) unless their whole wave is idle.
+template <int FM, int P2, bool FUSED, bool HASH, bool POL = false>
 __device__ __forceinline__ void step_body(const StepParams& p) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   constexpr bool BOT = P2 == FS_P2_BOT;
@@ -1063,7 +1078,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   // is issued before tick t's output stores, so its wait does not drain them
   // (loads and stores retire in order on one vmcnt counter).
   const uint8_t* src = k == 0 ? p.p1 : p.p2;
-  const bool reads = k == 0 || P2 == FS_P2_EXTERNAL;
+  const bool reads = POL ? (k == 1 && P2 == FS_P2_EXTERNAL) : (k == 0 || P2 == FS_P2_EXTERNAL);
   auto fetch = [&](int t) -> uint32_t {
     if (!reads) return 0u;
     if constexpr (HASH) return hash_action(p.action_seed, a, p.t0 + (uint64_t)t, k);
@@ -1073,13 +1088,37 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   Lane L;
   load_lane<BOT>(L, p.st, a, k);
   uint32_t next = fetch(0);
+  if constexpr (POL) stage_policy(p.pol);
   stage_tables();
-  if (!active) return;
+  if constexpr (POL) {
+    if ((l & ~63) >= 2 * p.n_envs) return;  // the whole wave is past the last arena
+  } else {
+    if (!active) return;
+  }
   if constexpr (!FUSED) {
     if (p.active && !p.active[a]) return;  // fs_step_masked: this arena does not tick
   }
   L.ai = action_info(L.f.act);
-  if constexpr (FUSED) {
+  if constexpr (POL) {
+    const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
+    const uint32_t arena0 = (uint32_t)(l & ~63) >> 1;
+    uint32_t d0, d1;
+    policy_features(L, d0, d1);
+    for (int t = 0; t < p.n_steps; t++) {
+      const uint32_t act = next;
+      next = fetch(min(t + 1, p.n_steps - 1));
+      const PolicyOut po = policy_act(d0, d1, p.pol.seed, arena0, p.t0 + (uint64_t)t);
+      if (active) {
+        const uint32_t row = (uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a;
+        if (k == 0) {
+          if (p.pol.actions) p.pol.actions[row] = (uint8_t)po.action;
+          if (p.pol.logp) p.pol.logp[row] = po.logp;
+        }
+        env_step<FM, P2>(L, k == 0 ? po.action : act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
+      }
+      policy_features(L, d0, d1);
+    }
+  } else if constexpr (FUSED) {
     const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
     for (int t = 0; t < p.n_steps; t++) {
       const uint32_t act = next;
@@ -1090,7 +1129,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     uint32_t none = 0;
     env_step<FM, P2>(L, next & 7u, p, (uint32_t)a, none);
   }
-  store_lane<BOT>(L, p.st, a);
+  if (active) store_lane<BOT>(L, p.st, a);
 }
 
 template <int FM, int P2>
@@ -1106,6 +1145,11 @@ __global__ __launch_bounds__(256) void k_step_n(StepParams p) {
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n_hashed(StepParams p) {
   step_body<FM, P2, true, true>(p);
+}
+
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step_n_policy(StepParams p) {
+  step_body<FM, P2, true, false, true>(p);
 }
 
 // FootsiesEnv.reset (FE:482-515) / RESET (BC:143-146) / game start (BC:105-128)
@@ -1308,7 +1352,8 @@ static inline dim3 grid_for(int n) { return dim3((unsigned)((n + kBlock - 1) / k
 template <int FM, int P2>
 static void launch_step_p2(const StepParams& p, hipStream_t s) {
   const dim3 grid = grid_for(2 * p.n_envs), block(kBlock);
-  if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
+  if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
+  else if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
   else hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
 }

@@ -8,6 +8,10 @@ replayed: the loop then costs graph launches, not the ~20 kernel launches per st
 
 Graph replays do not advance the handle's host-side step counter (fs_steps_taken), which
 only the hashed-action stream and frame_delay > 0 read; use eager steps for those.
+
+:class:`FusedPolicyRollout` goes one step further: the actor runs inside the simulator's
+fused tick loop (fs_step_n_policy, csrc/fs_policy.h) as bf16 MFMAs, so a block of n
+policy-driven ticks is one kernel launch with the arena state in registers throughout.
 """
 import ctypes as C
 
@@ -103,3 +107,52 @@ class PolicyRollout:
     def replay(self, times=1):
         for _ in range(times):
             self.graph.replay()
+
+
+class FusedPolicyRollout:
+    """C5 in one launch per block of ticks: `actor` (the make_actor shape, 8-64-64-8 with tanh)
+    is evaluated in bf16 inside the simulator kernel, P1's action drawn from its softmax by
+    inverse CDF with a counter-based uniform of (seed, env, step).  P2 is whatever the handle
+    was created with (bot, noop, or `p2_actions` [n][N] per call for external)."""
+
+    def __init__(self, sim, actor, seed=0):
+        torch = _torch()
+        lin = [m for m in actor if isinstance(m, torch.nn.Linear)]
+        shapes = [tuple(m.weight.shape) for m in lin]
+        if shapes != [(64, N_FEATURES), (64, 64), (N_ACTIONS, 64)]:
+            raise ValueError("the fused actor is 8 -> 64 -> 64 -> 8; got %s" % (shapes,))
+        self.sim, self.seed = sim, int(seed) & (2**64 - 1)
+        with torch.no_grad():
+            self.params = [t.detach().to(device=sim.device, dtype=torch.float32).contiguous()
+                           for m in lin for t in (m.weight, m.bias)]
+
+    def refresh(self, actor):
+        """Copy new actor weights in (after an optimiser step); the buffers stay put."""
+        torch = _torch()
+        lin = [m for m in actor if isinstance(m, torch.nn.Linear)]
+        with torch.no_grad():
+            for dst, src in zip(self.params, [t for m in lin for t in (m.weight, m.bias)]):
+                dst.copy_(src)
+
+    def rollout(self, n, actions=None, logp=None, p2_actions=None, trajectory=None):
+        """n policy-driven ticks in one launch.  `actions` (uint8) / `logp` (float32) [n][N]
+        device tensors receive P1's samples (allocated when None; pass False to skip one).
+        Returns (actions, logp)."""
+        torch = _torch()
+        N, dev = self.sim.num_envs, self.sim.device
+        if actions is None:
+            actions = torch.empty((n, N), dtype=torch.uint8, device=dev)
+        if logp is None:
+            logp = torch.empty((n, N), dtype=torch.float32, device=dev)
+        w = self.params
+        pol = _abi.fs_policy(w1=w[0].data_ptr(), b1=w[1].data_ptr(), w2=w[2].data_ptr(), b2=w[3].data_ptr(),
+                             w3=w[4].data_ptr(), b3=w[5].data_ptr(), seed=self.seed,
+                             actions_out=actions.data_ptr() if actions is not False else None,
+                             logp_out=logp.data_ptr() if logp is not False else None)
+        t = None
+        if trajectory is not None:
+            t = _abi.fs_outputs(**{k: trajectory[k].data_ptr() for k in _abi.OUTPUT_SPEC if k in trajectory})
+        check(lib().fs_step_n_policy(self.sim.handle, int(n), C.byref(pol),
+                                     None if p2_actions is None else C.c_void_p(p2_actions.data_ptr()),
+                                     None if t is None else C.byref(t)), self.sim.handle)
+        return actions, logp

@@ -208,6 +208,30 @@ int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, co
 int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act,
               uint64_t action_seed, const fs_outputs* traj);
 
+/* The actor of fs_step_n_policy: an MLP 8 -> 64 -> tanh -> 64 -> tanh -> 8 on
+ * P1's observation features [guard/3, move/16, move_frame/55, position/4.6] of
+ * P1 then P2 (footsies_gym_amd/rollout.py obs_features), fp32 device weights in
+ * torch nn.Linear layouts (weight [out][in]), computed in bf16 with f32
+ * accumulation.  The action is drawn from softmax(logits) by inverse CDF with
+ * u = uniform(seed, env, t) (fs_policy.h policy_uniform), t = fs_steps_taken + k. */
+typedef struct fs_policy {
+  const float* w1; /* [64][8] */
+  const float* b1; /* [64] */
+  const float* w2; /* [64][64] */
+  const float* b2; /* [64] */
+  const float* w3; /* [8][64] */
+  const float* b3; /* [8] */
+  uint64_t seed;
+  uint8_t* actions_out; /* [n][N] device: P1's sampled actions, or NULL */
+  float* logp_out;      /* [n][N] device: their log-probabilities, or NULL */
+} fs_policy;
+
+/* fs_step_n with P1 driven by the actor `pol` inside the fused tick loop: the
+ * whole policy-in-the-loop rollout in one launch.  p2_act:
+ * device [n][N] for FS_P2_EXTERNAL, ignored otherwise.  traj as in fs_step_n.
+ * FS_E_UNSUPPORTED with frame_delay > 0. */
+int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint8_t* p2_act, const fs_outputs* traj);
+
 /* Fill device arrays p1_out/p2_out [n_steps][N] with the synthetic action stream
  * of fs_step_n (splitmix64 hash of (seed, env, t0 + k, player)),
  * so benchmark inputs are resident in HBM before the timed region.
