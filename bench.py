@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="arenas per GPU")
     ap.add_argument("--mode", choices=["fused", "step"], default="fused")
-    ap.add_argument("--chunk", type=int, default=100, help="ticks per fs_step_n launch (fused mode)")
+    ap.add_argument("--chunk", type=int, default=1000, help="ticks per fs_step_n launch (fused mode; SURVEY 8(d) C3: n=1000)")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -66,10 +66,22 @@ def cpu_baseline(envs, seconds, seed):
     t = time.perf_counter()
     o.step_n_hashed(steps, seed)
     dt = time.perf_counter() - t
+    # the same port on one thread (SURVEY.md 8(d) asks for both), a short sample
+    binding.lib().or_set_threads(1)
+    t = time.perf_counter()
+    o.step_n_hashed(2, seed)
+    probe1 = time.perf_counter() - t
+    steps1 = int(max(2, min(100000, 0.2 * seconds / max(probe1 / 2, 1e-9))))
+    t = time.perf_counter()
+    o.step_n_hashed(steps1, seed)
+    dt1 = time.perf_counter() - t
+    binding.lib().or_set_threads(threads)
     o.close()
     return {"value": envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": "%d arenas x %d steps, self-play splitmix64 actions, oracle/liboracle.so (OpenMP %d threads), "
-                      "%.1f s" % (envs, steps, threads, dt)}
+                      "%.1f s" % (envs, steps, threads, dt),
+            "single_thread": {"value": envs * steps1 / dt1, "cores": 1,
+                              "sample": "%d arenas x %d steps, 1 thread, %.1f s" % (envs, steps1, dt1)}}
 
 
 def bot_mode_rate(torch, N, K, W, chunk, seed, device):
@@ -317,7 +329,7 @@ def main():
         except Exception as e:  # reported, never fatal to the headline measurement
             out["policy_loop"] = {"error": "%s: %s" % (type(e).__name__, e)}
         try:
-            out["policy_loop_fused"] = fused_policy_rate(torch, N, max(K * chunk // 10, 1000), local)
+            out["policy_loop_fused"] = fused_policy_rate(torch, N, 5 * chunk, local, ticks=chunk)
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             out["policy_loop_fused"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

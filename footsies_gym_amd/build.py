@@ -20,8 +20,11 @@ HEADERS = ["fs_internal.h", "fs_tables.h", "fs_policy.h"]
 # -simplifycfg-sink-common=false: SimplifyCFG otherwise sinks the per-branch field stores
 #   of the action state machine into one store through a pointer phi, which blocks SROA and
 #   leaves the whole per-lane arena (272 B) in scratch memory -- 400+ scratch ops per tick.
+# -amdgpu-mfma-vgpr-form: the policy kernel's MFMA results land in VGPRs, where the tanh
+#   epilogue reads them, instead of AGPRs plus one v_accvgpr_read per element.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
-          "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-bitwise-instead-of-logical", "-mllvm", "-simplifycfg-sink-common=false"]
+          "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-bitwise-instead-of-logical",
+          "-mllvm", "-simplifycfg-sink-common=false", "-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 
 def _hipcc():

@@ -9,8 +9,9 @@
 // its column (arena) on the lane and its rows in the 16 accumulator registers, which is the B
 // fragment of the next product with no data movement (the k order inside a fragment is
 // permuted -- element j of lane half h is row 16s + 8(j>>2) + 4h + (j&3) -- so the weight
-// fragments are built in that order).  Biases ride as an extra k slot against a constant 1.
-// Weights and inputs are rounded to bf16; accumulation is f32.
+// fragments are built in that order).  tanh's scale and offset are folded into the weights (see
+// kTanhScale), so a hidden value costs v_exp_f32 + v_add + v_rcp_f32 + half a v_cvt_pk_bf16_f32.
+// Weights, inputs and the hidden r values are bf16; accumulation is f32.
 //
 // MFMA operand maps (gfx950, 32x32x16 bf16): lane l, r = l & 31, h = l >> 5 holds
 // A[row r][k = 8h + j] and B[k = 8h + j][col r] in element j; C/D: col = r,
@@ -33,55 +34,72 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // hidden unit held in element j of a fragment built from accumulator registers 8s..8s+7
 __device__ __forceinline__ int acc_row(int s, int j, int h) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
 
+// tanh z = 1 - 2 r with r = 1 / (1 + 2^(c z)), c = 2 log2(e).  The affine parts are folded into
+// the weights: a layer whose output feeds tanh is pre-scaled by c, so its accumulator is the exp2
+// argument; a layer whose input is tanh of the previous one takes r instead, with weights -2 W
+// and bias b + sum_k W[., k] (so W (1 - 2 r) + b is unchanged).  What crosses between layers is
+// r rounded to bf16.  Biases ride in two k slots as a bf16 hi + lo pair against constant 1s.
+constexpr float kTanhScale = 2.8853900817779268f;  // 2 log2(e)
+
+__device__ __forceinline__ void bias_pair(bf16x8& a, float b) {
+  const __bf16 hi = (__bf16)b;
+  a[0] = hi;
+  a[1] = (__bf16)(b - (float)hi);
+}
+
 // Build the weight fragments once per block (threads 0..63 write; the caller syncs).
 __device__ __forceinline__ void stage_policy(const PolicyParams& P) {
   if (threadIdx.x >= 64) return;
   const int l = threadIdx.x, r = l & 31, h = l >> 5;
-  for (int t = 0; t < 2; t++) {  // layer 1: row = hidden 32t + r; k = feature 8h + j, k = 8 is the bias
-    bf16x8 a;
-    for (int j = 0; j < 8; j++)
-      a[j] = (__bf16)(h == 0 ? P.w1[(32 * t + r) * 8 + j] : (j == 0 ? P.b1[32 * t + r] : 0.0f));
+  for (int t = 0; t < 2; t++) {  // layer 1: row = hidden 32t + r; k = feature 8h + j, bias at k = 8, 9
+    bf16x8 a = {};
+    const int row = 32 * t + r;
+    if (h == 0)
+      for (int j = 0; j < 8; j++) a[j] = (__bf16)(kTanhScale * P.w1[row * 8 + j]);
+    else
+      bias_pair(a, kTanhScale * P.b1[row]);
     sPol[kPolA1 + t][l] = a;
   }
   for (int u = 0; u < 2; u++) {  // layer 2: row = hidden 32u + r; k = hidden 32t + acc_row(s, j, h)
+    const int row = 32 * u + r;
     for (int t = 0; t < 2; t++)
       for (int s = 0; s < 2; s++) {
         bf16x8 a;
-        for (int j = 0; j < 8; j++) a[j] = (__bf16)P.w2[(32 * u + r) * 64 + 32 * t + acc_row(s, j, h)];
+        for (int j = 0; j < 8; j++) a[j] = (__bf16)(-2.0f * kTanhScale * P.w2[row * 64 + 32 * t + acc_row(s, j, h)]);
         sPol[kPolA2 + 4 * u + 2 * t + s][l] = a;
       }
+    float sum = 0.0f;
+    for (int k = 0; k < 64; k++) sum += P.w2[row * 64 + k];
     bf16x8 b = {};
-    if (h == 0) b[0] = (__bf16)P.b2[32 * u + r];
+    if (h == 0) bias_pair(b, kTanhScale * (P.b2[row] + sum));
     sPol[kPolA2b + u][l] = b;
   }
   for (int u = 0; u < 2; u++)  // layer 3: row = action r (< 8, the rest zero); k = hidden 32u + ...
     for (int s = 0; s < 2; s++) {
       bf16x8 a;
-      for (int j = 0; j < 8; j++) a[j] = (__bf16)(r < 8 ? P.w3[r * 64 + 32 * u + acc_row(s, j, h)] : 0.0f);
+      for (int j = 0; j < 8; j++) a[j] = (__bf16)(r < 8 ? -2.0f * P.w3[r * 64 + 32 * u + acc_row(s, j, h)] : 0.0f);
       sPol[kPolA3 + 2 * u + s][l] = a;
     }
+  float sum = 0.0f;
+  if (r < 8)
+    for (int k = 0; k < 64; k++) sum += P.w3[r * 64 + k];
   bf16x8 b = {};
-  if (h == 0 && r < 8) b[0] = (__bf16)P.b3[r];
+  if (h == 0 && r < 8) bias_pair(b, P.b3[r] + sum);
   sPol[kPolA3b][l] = b;
 }
 
-// e^x on v_exp_f32 (2^x, ~1 ulp) with no denormal range fix-up: the results here are rounded
-// to bf16 or feed a softmax, so flushing tiny values is harmless
+// e^x on v_exp_f32 (2^x, ~1 ulp) with no denormal range fix-up: the results feed a softmax
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
-// tanh x = 1 - 2 / (1 + e^(2x)) with v_rcp_f32 (~1 ulp) for the division: 5 VALU ops, saturates
-// to +-1 through e = inf / 0 (no NaN for finite x); the result is rounded to bf16 next
-__device__ __forceinline__ float fast_tanh(float x) {
-  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
-  return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
-}
-
-// one hidden tile: tanh of the accumulator, packed as the two B fragments (k-steps s = 0, 1)
+// one hidden tile: r = 1 / (1 + 2^d) of the (pre-scaled) accumulator on v_exp_f32 / v_rcp_f32
+// (~1 ulp each; saturates through 2^d = inf / 0, no NaN for finite d), packed as the two B
+// fragments (k-steps s = 0, 1) of the next layer
+__device__ __forceinline__ float tanh_r(float d) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(d)); }
 __device__ __forceinline__ void activate(const f32x16& d, bf16x8& b0, bf16x8& b1) {
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    b0[j] = (__bf16)fast_tanh(d[j]);
-    b1[j] = (__bf16)fast_tanh(d[8 + j]);
+    b0[j] = (__bf16)tanh_r(d[j]);
+    b1[j] = (__bf16)tanh_r(d[8 + j]);
   }
 }
 
@@ -131,11 +149,11 @@ __device__ __forceinline__ PolicyOut policy_act(uint32_t d0, uint32_t d1, uint64
     v.y = __builtin_amdgcn_perm(p2d0, p1d0, 0x07060302u);  // hi halves: m1 | m2
     v.z = __builtin_amdgcn_perm(p2d1, p1d1, 0x05040100u);
     v.w = __builtin_amdgcn_perm(p2d1, p1d1, 0x07060302u);
-    const u32x4 one = {0x3F80u, 0u, 0u, 0u};  // k = 8: bf16 1.0 (the layer-1 bias slot)
+    const u32x4 one = {0x3F803F80u, 0u, 0u, 0u};  // k = 8, 9: bf16 1.0 (the layer-1 bias pair)
     x = __builtin_bit_cast(bf16x8, h == 0 ? v : one);
   }
-  bf16x8 ones = {};
-  if (h == 0) ones[0] = (__bf16)1.0f;
+  bf16x8 ones = {};  // the bias pair's k slots of layers 2 and 3
+  if (h == 0) ones[0] = ones[1] = (__bf16)1.0f;
   const f32x16 zero = {};
   // layer 1
   f32x16 d1a = mfma(sPol[kPolA1 + 0][l], x, zero), d1b = mfma(sPol[kPolA1 + 1][l], x, zero);
