@@ -285,6 +285,23 @@ def main():
             check(rc, h)
     torch.cuda.synchronize(dev)
     host_rate = N * kh / (time.perf_counter() - t0)
+    # the per-step path with the multi-GPU exchange of SURVEY 8(e): every step's outputs packed
+    # on device into 40-B records (fs_pack_outputs) and all-gathered over RCCL/xGMI, so every
+    # rank (a centralised learner on rank 0) holds the global batch; reported beside `value`
+    kg = min(K, 500)
+    rec = torch.empty((N, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=dev)
+    gbuf = torch.empty((world * N, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=dev)
+    fs_pack = L.fs_pack_outputs
+
+    def run_step_gather(k0, n):
+        for k in range(k0, k0 + n):
+            rc = fs_step(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE)
+            rc = rc or fs_pack(h, C.c_void_p(rec.data_ptr()))
+            if rc:
+                check(rc, h)
+            if world > 1:
+                dist.all_gather_into_tensor(gbuf, rec)
+    gwall, _ = timed(run_step_gather, W, kg)
     # dominant kernel of the reported mode, back-to-back launches
     if args.mode == "fused":
         kt, kmed = kernel_time(run_fused, W, max(5, args.kernel_samples // 10), chunk)
@@ -321,6 +338,10 @@ def main():
         other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
         "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
                                    "note": "fs_step with FS_ACT_HOST (PCIe-inclusive action hand-over)"},
+        "step_gather_mode": {"value": world * N * kg / gwall, "ms_per_step": 1e3 * gwall / kg, "steps": kg,
+                             "bytes_gathered_per_step": world * N * _abi.FS_RECORD_BYTES,
+                             "note": "fs_step + fs_pack_outputs + one all_gather_into_tensor of the 40-B "
+                                     "(obs, reward, done) records over RCCL per step (none at 1 GPU)"},
     }
     if world == 1 and not args.no_extras:
         out["p2_bot_mode"] = bot_mode_rate(torch, N, K, W, chunk, args.seed, local)

@@ -33,6 +33,7 @@ FS_RESET_HARD = 0
 FS_RESET_IF_NEEDED = 1
 FS_RESET_SEED_ONLY = 2
 FS_MAX_FRAME_DELAY = 4096
+FS_RECORD_BYTES = 40
 
 # InputDefine (Assets/Script/InputData.cs:8-14)
 IN_LEFT, IN_RIGHT, IN_ATTACK = 1, 2, 4
@@ -132,6 +133,7 @@ LIB_FUNCTIONS = {
     "fs_step_n_policy": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(fs_policy), C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_hash_actions": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "fs_outputs_get": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),
+    "fs_pack_outputs": (C.c_int, [C.c_void_p, C.c_void_p]),
     "fs_bind_outputs": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_get_env_state": (C.c_int, [C.c_void_p, C.POINTER(fs_env_state)]),
     "fs_get_state": (C.c_int, [C.c_void_p, C.POINTER(fs_arena_state)]),

@@ -399,6 +399,15 @@ FS_API int fs_outputs_get(fs_handle h, fs_outputs* o) {
   return FS_OK;
 }
 
+FS_API int fs_pack_outputs(fs_handle h, void* dst) {
+  if (!h) return FS_E_INVALID;
+  if (!dst) return set_err(h, FS_E_INVALID, "fs_pack_outputs: destination required");
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  HIP_TRY(h, fsk::launch_pack_records(h->out, dst, h->n, h->stream));
+  return FS_OK;
+}
+
 FS_API int fs_bind_outputs(fs_handle h, const fs_outputs* dev) {
   if (!h) return FS_E_INVALID;
   outputs_from_own(h);

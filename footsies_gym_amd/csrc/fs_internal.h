@@ -100,5 +100,6 @@ hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_stat
                             hipStream_t s);
 hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, int p2_mode, hipStream_t s);
 hipError_t launch_delay(const DelayParams& p, hipStream_t s);
+hipError_t launch_pack_records(const DevOutputs& o, void* dst, int n, hipStream_t s);
 
 }  // namespace fsk

@@ -53,14 +53,13 @@ def unpack_outputs(rec, torch):
     }
 
 
-def gather_outputs(out, group=None, shard_sizes=None):
-    """All-gather every rank's per-arena outputs into global-index order (one collective).
-
-    `shard_sizes` (per rank) handles uneven shards by padding to the largest."""
+def gather_records(rec, group=None, shard_sizes=None):
+    """All-gather every rank's packed [n, RECORD_BYTES] records into global-index order (one
+    all_gather over RCCL/xGMI, or gloo on CPU).  `shard_sizes` (per rank) handles uneven shards
+    by padding to the largest.  Returns the [global_envs, RECORD_BYTES] records."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    rec = pack_outputs(out, torch)
     n = rec.shape[0]
     sizes = shard_sizes or [n] * world
     m = max(sizes)
@@ -68,8 +67,16 @@ def gather_outputs(out, group=None, shard_sizes=None):
         rec = torch.cat([rec, torch.zeros((m - n, RECORD_BYTES), dtype=rec.dtype, device=rec.device)])
     buf = torch.empty((world * m, RECORD_BYTES), dtype=rec.dtype, device=rec.device)
     dist.all_gather_into_tensor(buf, rec, group=group)
-    parts = [buf[r * m: r * m + sizes[r]] for r in range(world)]
-    return unpack_outputs(torch.cat(parts), torch)
+    if all(sz == m for sz in sizes):
+        return buf
+    return torch.cat([buf[r * m: r * m + sizes[r]] for r in range(world)])
+
+
+def gather_outputs(out, group=None, shard_sizes=None):
+    """All-gather every rank's per-arena outputs dict (torch tensors, any device) into
+    global-index order: packed by `pack_outputs`, then `gather_records`."""
+    import torch
+    return unpack_outputs(gather_records(pack_outputs(out, torch), group, shard_sizes), torch)
 
 
 class ShardedSim:
@@ -85,7 +92,10 @@ class ShardedSim:
         return self.sim.step(p1, p2)
 
     def gather(self, group=None):
-        return gather_outputs(self.sim.outputs(), group, self.sizes)
+        """Every rank's outputs in global-index order: the records packed on device by
+        fs_pack_outputs, then one all_gather."""
+        import torch
+        return unpack_outputs(gather_records(self.sim.pack_outputs(), group, self.sizes), torch)
 
     def close(self):
         self.sim.close()

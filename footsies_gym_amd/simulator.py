@@ -179,6 +179,15 @@ class FootsiesSim:
     def outputs(self):
         return self._out
 
+    def pack_outputs(self, dst=None):
+        """The current outputs as one 40-byte record per arena ([N, 40] uint8 device tensor,
+        parallel.RECORD_BYTES layout) by one kernel (fs_pack_outputs): the gather payload."""
+        torch = _torch()
+        if dst is None:
+            dst = torch.empty((self.num_envs, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=self.device)
+        check(lib().fs_pack_outputs(self._h, C.c_void_p(dst.data_ptr())), self._h)
+        return dst
+
     def outputs_numpy(self):
         _torch().cuda.synchronize(self.device)
         return {k: v.cpu().numpy() for k, v in self._out.items()}

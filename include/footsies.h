@@ -241,6 +241,13 @@ int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_
 /* Device pointers of the current outputs, valid until the next call on h. */
 int fs_outputs_get(fs_handle h, fs_outputs* out);
 
+/* Pack the current outputs into one FS_RECORD_BYTES record per arena at dst (device,
+ * [N][40] bytes): guard[2] move[2] action[2] hitstun[2] u8, terminated u8, truncated
+ * u8, pad[2], move_frame[2] f32, position[2] f32, frame i32, reward f64 -- the payload
+ * of the multi-GPU per-step gather over RCCL.  Asynchronous. */
+#define FS_RECORD_BYTES 40
+int fs_pack_outputs(fs_handle h, void* dst);
+
 /* Redirect the per-step outputs into caller-owned device buffers (e.g. torch
  * tensors) for zero-copy; NULL members keep the library's own buffer.  The
  * buffers must stay alive until fs_destroy or the next bind. */

@@ -378,3 +378,25 @@ def test_single_env_adapter_matches_reference_api():
     obs, info = env.reset()
     assert info["frame"] == -1
     env.close()
+
+
+def test_pack_outputs_kernel_matches_host_packing():
+    """fs_pack_outputs (one kernel) == parallel.pack_outputs (torch ops) byte for byte, and
+    ShardedSim.gather's unpacking restores the outputs."""
+    import torch
+    from footsies_gym_amd import parallel
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(1003, p2_mode="external", seed=2)
+    p1, p2 = sim.hash_actions(300, seed=9)
+    terminals = 0
+    for t in range(300):
+        sim.step(p1[t], p2[t])
+        if t >= 100:
+            got = sim.pack_outputs()
+            want = parallel.pack_outputs(sim.outputs(), torch)
+            assert bool(torch.equal(got, want)), t
+            terminals += int(sim.outputs()["terminated"].sum())
+    assert terminals > 0  # terminal rows covered
+    back = parallel.unpack_outputs(got, torch)
+    for k, v in back.items():
+        assert bool(torch.equal(v, sim.outputs()[k])), k
