@@ -46,29 +46,7 @@ constexpr uint32_t IN_LEFT = 1, IN_RIGHT = 2, IN_ATTACK = 4;
 // ---------------------------------------------------------------------------
 __shared__ Tables sT;
 
-// Copy the kTables image (fs_tables.h) into LDS: every thread issues all of its
-// loads before any store, so the block waits for one round trip, not one per table.
-// All threads of the block must call this before any early return.
 constexpr int kBlock = 256;
-__device__ __forceinline__ void stage_tables() {
-  constexpr int kWords = sizeof(Tables) / 4;
-  constexpr int kPer = (kWords + kBlock - 1) / kBlock;
-  static_assert(sizeof(Tables) % 4 == 0, "table image must be word-sized");
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(&kTables);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(&sT);
-  uint32_t v[kPer];
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const int i = threadIdx.x + j * kBlock;
-    v[j] = i < kWords ? src[i] : 0u;
-  }
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const int i = threadIdx.x + j * kBlock;
-    if (i < kWords) dst[i] = v[j];
-  }
-  __syncthreads();
-}
 
 // ---------------------------------------------------------------------------
 // packed fighter word (u64), one per fighter in DevState::fpk
@@ -544,11 +522,11 @@ __device__ __forceinline__ HitTest resolve(const BoxHits& r, int att_hits) {
 // ---------------------------------------------------------------------------
 enum { MP_NEUTRAL, MP_FAR1, MP_FAR2, MP_MID1, MP_MID2, MP_FALLBACK1, MP_FALLBACK2 };
 enum { AP_NONE, AP_ONE_HIT, AP_TWO_HIT, AP_IMMEDIATE_SPECIAL, AP_DELAY_SPECIAL };
-__device__ __forceinline__ uint32_t move_plan_len(uint32_t plan) {  // AI:192-253
+constexpr uint32_t move_plan_len(uint32_t plan) {  // AI:192-253
   return plan == MP_FAR1 ? 90u : plan == MP_FAR2 ? 56u : plan == MP_MID1 ? 70u : plan == MP_MID2 ? 33u
        : plan == MP_FALLBACK1 ? 60u : plan == MP_FALLBACK2 ? 63u : 30u;
 }
-__device__ __forceinline__ uint32_t attack_plan_len(uint32_t plan) {  // AI:255-312
+constexpr uint32_t attack_plan_len(uint32_t plan) {  // AI:255-312
   return plan == AP_ONE_HIT ? 19u : plan == AP_TWO_HIT ? 23u : plan == AP_IMMEDIATE_SPECIAL ? 61u
        : plan == AP_DELAY_SPECIAL ? 121u : 30u;
 }
@@ -561,9 +539,6 @@ __device__ __forceinline__ uint32_t rng_next(uint4& s) {  // UnityEngine.Random 
   s.w = s.w ^ (s.w >> 19) ^ t ^ (t >> 8);
   return s.w;
 }
-__device__ __forceinline__ int rng_range(uint4& s, int mn, int mx) {  // Random.Range(int, int)
-  return mn + (int)(rng_next(s) % (uint32_t)(mx - mn));
-}
 __device__ __forceinline__ uint4 rng_init(int32_t seed) {  // Random.InitState
   uint4 s;
   s.x = (uint32_t)seed;
@@ -575,7 +550,7 @@ __device__ __forceinline__ uint4 rng_init(int32_t seed) {  // Random.InitState
 
 // P2's forward is Left, backward is Right (AI:380-388); the dash plans are
 // [F, 0, F] -- AddBackwardDashInputQueue also enqueues forward (AI:337-342).
-__device__ __forceinline__ uint32_t move_plan_input(uint32_t plan, uint32_t i) {
+constexpr uint32_t move_plan_input(uint32_t plan, uint32_t i) {
   const uint32_t F = IN_LEFT, B = IN_RIGHT;
   switch (plan) {
     case MP_FAR1: return i < 40 ? F : i < 50 ? B : i < 80 ? F : B;
@@ -590,51 +565,114 @@ __device__ __forceinline__ uint32_t move_plan_input(uint32_t plan, uint32_t i) {
     default: return 0u;  // MP_NEUTRAL
   }
 }
-__device__ __forceinline__ uint32_t attack_plan_input(uint32_t plan, uint32_t i) {
-  switch (plan) {
-    case AP_ONE_HIT: return i == 0 ? IN_ATTACK : 0u;
-    case AP_TWO_HIT: return (i == 0 || i == 4) ? IN_ATTACK : 0u;
-    case AP_IMMEDIATE_SPECIAL: return i < 60 ? IN_ATTACK : 0u;
-    case AP_DELAY_SPECIAL: return i < 120 ? IN_ATTACK : 0u;
-    default: return 0u;
-  }
+// frames at the start of an attack plan with Attack held; AP_TWO_HIT also presses at index 4
+constexpr uint32_t attack_plan_hold(uint32_t plan) {  // AI:255-312
+  return plan == AP_ONE_HIT || plan == AP_TWO_HIT ? 1u : plan == AP_IMMEDIATE_SPECIAL ? 60u
+       : plan == AP_DELAY_SPECIAL ? 120u : 0u;
 }
 
-__device__ __forceinline__ uint32_t select_movement(uint4& rng, float d) {  // AI:68-126
-  if (d > 4.0f) return rng_range(rng, 0, 2) == 0 ? MP_FAR1 : MP_FAR2;
-  if (d > 3.0f) {
-    const int r = rng_range(rng, 0, 7);
-    return r <= 1 ? MP_MID1 : r <= 3 ? MP_MID2 : r == 4 ? MP_FAR1 : r == 5 ? MP_FAR2 : MP_NEUTRAL;
+// The plan choices as (n, outcome of Random.Range(0, n) = r) per distance bucket
+// b = [d > 4, d > 3, d > 2.5, d > 2, else] (SelectMovement AI:68-126, SelectAttack AI:128-190).
+constexpr uint32_t move_draw_n(int b) { return b == 0 ? 2u : b == 1 ? 7u : b == 2 ? 5u : b == 3 ? 4u : 3u; }
+constexpr uint32_t move_draw_plan(int b, uint32_t r) {
+  switch (b) {
+    case 0: return r == 0 ? MP_FAR1 : MP_FAR2;
+    case 1: return r <= 1 ? MP_MID1 : r <= 3 ? MP_MID2 : r == 4 ? MP_FAR1 : r == 5 ? MP_FAR2 : MP_NEUTRAL;
+    case 2: return r == 0 ? MP_MID1 : r == 1 ? MP_MID2 : r == 2 ? MP_FALLBACK1 : r == 3 ? MP_FALLBACK2 : MP_NEUTRAL;
+    case 3: return r == 0 ? MP_FALLBACK1 : r == 1 ? MP_FALLBACK2 : MP_NEUTRAL;
+    default: return r == 0 ? MP_FALLBACK1 : r == 1 ? MP_FALLBACK2 : MP_NEUTRAL;
   }
-  if (d > 2.5f) {
-    const int r = rng_range(rng, 0, 5);
-    return r == 0 ? MP_MID1 : r == 1 ? MP_MID2 : r == 2 ? MP_FALLBACK1 : r == 3 ? MP_FALLBACK2 : MP_NEUTRAL;
+}
+constexpr uint32_t attack_draw_n(int b) { return b == 0 ? 4u : b == 1 ? 5u : b == 2 ? 3u : b == 3 ? 6u : 3u; }
+constexpr uint32_t attack_draw_plan(int b, uint32_t r) {
+  switch (b) {
+    case 0: return r <= 3 ? AP_NONE : AP_DELAY_SPECIAL;
+    case 1: return r <= 1 ? AP_NONE : r <= 3 ? AP_ONE_HIT : AP_DELAY_SPECIAL;
+    case 2: return r == 0 ? AP_NONE : r == 1 ? AP_ONE_HIT : AP_TWO_HIT;
+    case 3: return r <= 1 ? AP_ONE_HIT : r <= 3 ? AP_TWO_HIT : r == 4 ? AP_IMMEDIATE_SPECIAL : AP_DELAY_SPECIAL;
+    default: return r == 0 ? AP_ONE_HIT : AP_TWO_HIT;
   }
-  if (d > 2.0f) {
-    const int r = rng_range(rng, 0, 4);
-    return r == 0 ? MP_FALLBACK1 : r == 1 ? MP_FALLBACK2 : MP_NEUTRAL;
-  }
-  const int r = rng_range(rng, 0, 3);
-  return r == 0 ? MP_FALLBACK1 : r == 1 ? MP_FALLBACK2 : MP_NEUTRAL;
+}
+// SelectAttack's answers that take no Random.Range draw: a hit/special/guard-break opponent
+// (any distance), or an attacking one at 3 < d <= 4
+__device__ __forceinline__ bool attack_forced(uint32_t b, uint32_t opp) {
+  constexpr uint32_t kAny = (1u << A_DAMAGE) | (1u << A_GUARD_BREAK) | (1u << A_N_SPECIAL) | (1u << A_B_SPECIAL);
+  constexpr uint32_t kMid = (1u << A_N_ATTACK) | (1u << A_B_ATTACK);
+  return (((b == 1 ? kAny | kMid : kAny) >> opp) & 1u) != 0;
 }
 
-__device__ __forceinline__ uint32_t select_attack(uint4& rng, float d, uint32_t opp) {  // AI:128-190
-  if (opp == A_DAMAGE || opp == A_GUARD_BREAK || opp == A_N_SPECIAL || opp == A_B_SPECIAL) return AP_TWO_HIT;
-  if (d > 4.0f) return rng_range(rng, 0, 4) <= 3 ? AP_NONE : AP_DELAY_SPECIAL;
-  if (d > 3.0f) {
-    if (opp == A_N_ATTACK || opp == A_B_ATTACK) return AP_TWO_HIT;
-    const int r = rng_range(rng, 0, 5);
-    return r <= 1 ? AP_NONE : r <= 3 ? AP_ONE_HIT : AP_DELAY_SPECIAL;
+// The bot as tables (staged into LDS with the frame data): plan inputs as 2-bit codes,
+// one draw descriptor per bucket, plan lengths.
+struct alignas(16) BotDraw {
+  uint32_t map;    // nibble r = the plan drawn for r
+  uint32_t magic;  // ceil(2^32 / n): r = v - n * umulhi(v, magic) is exact for v < 2^20
+  uint32_t n;
+  uint32_t c16;    // 65536 % n
+};
+struct alignas(16) BotTables {
+  BotDraw move[5], attack[5];
+  uint32_t move_codes[7][6];  // plan p, index i: input bits at 2 (i & 15) of word i >> 4
+  uint8_t move_len[8], attack_len[8], attack_hold[8];
+  uint32_t pad[2];
+};
+constexpr BotDraw make_draw(uint32_t n, uint32_t map) {
+  return BotDraw{map, (uint32_t)((0x100000000ull + n - 1) / n), n, 65536u % n};
+}
+constexpr BotTables make_bot_tables() {
+  BotTables t{};
+  for (int b = 0; b < 5; b++) {
+    uint32_t mm = 0, ma = 0;
+    for (uint32_t r = 0; r < move_draw_n(b); r++) mm |= move_draw_plan(b, r) << (4 * r);
+    for (uint32_t r = 0; r < attack_draw_n(b); r++) ma |= attack_draw_plan(b, r) << (4 * r);
+    t.move[b] = make_draw(move_draw_n(b), mm);
+    t.attack[b] = make_draw(attack_draw_n(b), ma);
   }
-  if (d > 2.5f) {
-    const int r = rng_range(rng, 0, 3);
-    return r == 0 ? AP_NONE : r == 1 ? AP_ONE_HIT : AP_TWO_HIT;
+  for (uint32_t p = 0; p < 7; p++) {
+    t.move_len[p] = (uint8_t)move_plan_len(p);
+    for (uint32_t i = 0; i < move_plan_len(p); i++) t.move_codes[p][i >> 4] |= move_plan_input(p, i) << (2 * (i & 15));
   }
-  if (d > 2.0f) {
-    const int r = rng_range(rng, 0, 6);
-    return r <= 1 ? AP_ONE_HIT : r <= 3 ? AP_TWO_HIT : r == 4 ? AP_IMMEDIATE_SPECIAL : AP_DELAY_SPECIAL;
+  for (uint32_t p = 0; p < 5; p++) {
+    t.attack_len[p] = (uint8_t)attack_plan_len(p);
+    t.attack_hold[p] = (uint8_t)attack_plan_hold(p);
   }
-  return rng_range(rng, 0, 3) == 0 ? AP_ONE_HIT : AP_TWO_HIT;
+  return t;
+}
+static_assert(move_plan_len(MP_FAR1) <= 6 * 16, "move plans fit six code words");
+__constant__ const BotTables kBot = make_bot_tables();
+__shared__ BotTables sBot;
+
+// Copy the kTables image (fs_tables.h) and the bot tables into LDS: every thread issues all
+// of its loads before any store, so the block waits for one round trip, not one per table.
+// All threads of the block must call this before any early return.
+__device__ __forceinline__ void stage_tables() {
+  constexpr int kWords = sizeof(Tables) / 4;
+  constexpr int kPer = (kWords + kBlock - 1) / kBlock;
+  static_assert(sizeof(Tables) % 4 == 0, "table image must be word-sized");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&kTables);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&sT);
+  uint32_t v[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int i = threadIdx.x + j * kBlock;
+    v[j] = i < kWords ? src[i] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int i = threadIdx.x + j * kBlock;
+    if (i < kWords) dst[i] = v[j];
+  }
+  constexpr int kBotWords = sizeof(BotTables) / 4;
+  static_assert(kBotWords <= kBlock, "one bot-table word per thread");
+  if (threadIdx.x < kBotWords)
+    reinterpret_cast<uint32_t*>(&sBot)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&kBot)[threadIdx.x];
+  __syncthreads();
+}
+
+// Random.Range(0, n) = x % n for the draw descriptor: x = h 2^16 + l, so x % n = (h (2^16 % n) + l) % n
+// with the inner value < 2^20, where the magic multiply is exact
+__device__ __forceinline__ uint32_t draw_mod(uint32_t x, const BotDraw& d) {
+  const uint32_t v = (x >> 16) * d.c16 + (x & 0xFFFFu);
+  return v - d.n * __umulhi(v, d.magic);
 }
 
 // getNextAIInput (AI:41-66) for the P2 bot.  The ascending copy loop of
@@ -642,7 +680,7 @@ __device__ __forceinline__ uint32_t select_attack(uint4& rng, float d, uint32_t 
 // state, so the bot keeps one FightState: (distance, opponent action).
 struct Bot {
   uint4 rng;
-  uint32_t mplan, midx, aplan, aidx, prev_opp;
+  uint32_t mplan, midx, aplan, aidx, prev_opp;  // plans stored + 1 (0 = queue empty)
   float prev_dist;
 };
 
@@ -652,26 +690,37 @@ __device__ __forceinline__ float bot_distance(float x1, float x2) {
   return fabsf(fsub<FM>(x2, x1));
 }
 
+// Branch-free: both queues' next inputs from the code tables, both possible draws computed
+// (movement first, then attack -- the order the C# calls Random.Range) and the RNG state
+// advanced by the number actually taken.
 __device__ __forceinline__ uint32_t bot_next_input(Bot& b, float dist, uint32_t opp_act) {
   const float d = b.prev_dist;
   const uint32_t opp = b.prev_opp;
   b.prev_dist = dist;
   b.prev_opp = opp_act;
-  uint32_t input = 0;
-  if (b.mplan) {
-    input |= move_plan_input(b.mplan - 1, b.midx);
-    if (++b.midx == move_plan_len(b.mplan - 1)) b.mplan = 0;
-  } else {
-    b.mplan = select_movement(b.rng, d) + 1;
-    b.midx = 0;
-  }
-  if (b.aplan) {
-    input |= attack_plan_input(b.aplan - 1, b.aidx);
-    if (++b.aidx == attack_plan_len(b.aplan - 1)) b.aplan = 0;
-  } else {
-    b.aplan = select_attack(b.rng, d, opp) + 1;
-    b.aidx = 0;
-  }
+  const uint32_t bucket = d > 4.0f ? 0u : d > 3.0f ? 1u : d > 2.5f ? 2u : d > 2.0f ? 3u : 4u;
+  const bool mbusy = b.mplan != 0, abusy = b.aplan != 0;
+  const uint32_t mp = mbusy ? b.mplan - 1 : 0u, ap = abusy ? b.aplan - 1 : 0u;
+  const uint32_t mi = b.midx, ai = b.aidx;
+  const uint32_t in_m = (sBot.move_codes[mp][mi >> 4] >> (2 * (mi & 15))) & 3u;
+  const bool press = (ai < sBot.attack_hold[ap]) | ((ap == AP_TWO_HIT) & (ai == 4));
+  const uint32_t input = (mbusy ? in_m : 0u) | ((abusy & press) ? IN_ATTACK : 0u);
+  const bool forced = attack_forced(bucket, opp);
+  const bool dm = !mbusy, da = !abusy & !forced;
+  uint4 s1 = b.rng;
+  const uint32_t x1 = rng_next(s1);
+  uint4 s2 = s1;
+  const uint32_t x2 = rng_next(s2);
+  const uint4 s0 = b.rng;
+  b.rng = (dm & da) ? s2 : (dm | da) ? s1 : s0;
+  const BotDraw wm = sBot.move[bucket], wa = sBot.attack[bucket];
+  const uint32_t new_m = (wm.map >> (4 * draw_mod(x1, wm))) & 15u;
+  const uint32_t new_a = forced ? (uint32_t)AP_TWO_HIT : (wa.map >> (4 * draw_mod(dm ? x2 : x1, wa))) & 15u;
+  const uint32_t mi1 = mi + 1, ai1 = ai + 1;
+  b.mplan = mbusy ? (mi1 == sBot.move_len[mp] ? 0u : b.mplan) : new_m + 1;
+  b.midx = mbusy ? mi1 : 0u;
+  b.aplan = abusy ? (ai1 == sBot.attack_len[ap] ? 0u : b.aplan) : new_a + 1;
+  b.aidx = abusy ? ai1 : 0u;
   return input;
 }
 
