@@ -38,7 +38,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--envs", type=int, default=65536, help="arenas per GPU")
+    ap.add_argument("--envs", type=int, default=65536, help="arenas per GPU (weak scaling)")
+    ap.add_argument("--global-envs", type=int, default=0,
+                    help="strong scaling: this many arenas in total, split evenly over the ranks "
+                         "(SURVEY 8(d) C4: 262144); overrides --envs")
     ap.add_argument("--mode", choices=["fused", "step"], default="fused")
     ap.add_argument("--chunk", type=int, default=1000, help="ticks per fs_step_n launch (fused mode; SURVEY 8(d) C3: n=1000)")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
@@ -198,6 +201,11 @@ def main():
     from footsies_gym_amd.simulator import FootsiesSim
 
     N, K, W = args.envs, args.steps, args.warmup
+    if args.global_envs:
+        if args.global_envs % world:
+            raise SystemExit("--global-envs must be a multiple of the rank count")
+        N = args.global_envs // world
+    scaling = "strong" if args.global_envs else "weak"
     sim = FootsiesSim(N, device=local, p2_mode="external", seed=rank * N)
     h = sim.handle
     L = lib()
@@ -323,11 +331,12 @@ def main():
         "warmup": W,
         "ms_per_step": res[args.mode]["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int32+f32 (reward f64)",
         "data": "synthetic (splitmix64 self-play actions in HBM)",
-        "config": {"workload": "C3: %d arenas/GPU, self-play random actions, P2 external, auto-reset same-step" % N,
+        "config": {"workload": ("C4 strong: %d arenas over %d GPUs" % (N * world, world) if args.global_envs else
+                                "C3: %d arenas/GPU" % N) + ", self-play random actions, P2 external, auto-reset same-step",
                    "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
                    "ticks_per_launch": chunk if args.mode == "fused" else 1, "parallelism": "arena-shard x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",

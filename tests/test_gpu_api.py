@@ -400,3 +400,28 @@ def test_pack_outputs_kernel_matches_host_packing():
     back = parallel.unpack_outputs(got, torch)
     for k, v in back.items():
         assert bool(torch.equal(v, sim.outputs()[k])), k
+
+
+@pytest.mark.parametrize("extra", [[], ["--global-envs", "4096", "--mode", "step"]])
+def test_bench_json_contract(extra):
+    """bench.py prints one JSON line with the driver's fields, the roofline and (1 GPU) the
+    CPU baseline; --global-envs switches to strong scaling."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--envs", "4096", "--steps", "100", "--warmup", "10",
+           "--chunk", "50", "--no-extras", "--cpu-seconds", "0.5", "--kernel-samples", "10"] + extra
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True).stdout
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "step_gather_mode"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 100 and d["warmup"] == 10 and d["value"] > 0
+    assert d["scaling"] == ("strong" if extra else "weak")
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and 0 < r["frac"] < 1 and r["achieved"] == pytest.approx(r["frac"] * r["peak"])
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] >= 1
