@@ -425,3 +425,20 @@ def test_bench_json_contract(extra):
     r = d["roofline"]
     assert r["bound"] == "hbm" and 0 < r["frac"] < 1 and r["achieved"] == pytest.approx(r["frac"] * r["peak"])
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] >= 1
+
+
+def test_native_consumer_under_host_sanitizers():
+    """tests/native/abi_lockstep: a C++ program on include/footsies.h, built with host-side
+    ASan + UBSan over a sanitizer build of the library's host code, steps the GPU in lockstep
+    with the linked-in oracle (bitwise state compare), checks determinism across handles, the
+    packed gather records and the C-ABI's error paths."""
+    import os
+    import subprocess
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+    b = subprocess.run(["make", "-C", d, "-j4"], capture_output=True, text=True, timeout=900)
+    assert b.returncode == 0, b.stderr[-4000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="print_stacktrace=1",
+               LSAN_OPTIONS="suppressions=" + os.path.join(d, "lsan.supp"))
+    r = subprocess.run([os.path.join(d, "abi_lockstep")], env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "all checks passed" in r.stdout
