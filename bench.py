@@ -165,6 +165,23 @@ def fused_policy_rate(torch, N, steps, device, ticks=100):
                       "inverse-CDF sampling + log-prob stored per tick, P2 = bot" % N}
 
 
+def ppo_rate(torch, N, device, horizon=128, iterations=3):
+    """Config C5 end to end: PPO iterations (fused rollout of `horizon` ticks with the in-kernel
+    actor, then GAE and 2 epochs x 4 minibatches of fp32 torch updates of actor and critic,
+    then the new weights copied into the kernel's buffers); P2 = bot.  One untimed warm-up
+    iteration."""
+    from footsies_gym_amd.ppo import PPOTrainer
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
+    tr = PPOTrainer(sim, horizon=horizon)
+    tr.train(1)
+    rate = tr.train(iterations)
+    sim.close()
+    return {"value": rate, "horizon": horizon, "iterations": iterations,
+            "config": "C5 end to end: %d arenas, PPO (fused rollout of %d ticks + GAE + 2x4 Adam minibatch "
+                      "updates of the 8-64-64-8 actor and critic), P2 = bot" % (N, horizon)}
+
+
 def pmc_traffic(kernel, envs, ticks):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/*_traffic.json, written by tools/summarize_profile.py from separate
@@ -362,6 +379,10 @@ def main():
             out["policy_loop_fused"] = fused_policy_rate(torch, N, 5 * chunk, local, ticks=chunk)
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             out["policy_loop_fused"] = {"error": "%s: %s" % (type(e).__name__, e)}
+        try:
+            out["ppo_end_to_end"] = ppo_rate(torch, N, local)
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            out["ppo_end_to_end"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)
     if rank == 0:

@@ -1,0 +1,147 @@
+"""A small PPO learner over fused rollouts (BASELINE config C5: "65 536 envs driving a small
+PPO actor (PyTorch-ROCm), end-to-end steps/sec with policy in the loop").
+
+One iteration:
+1. `horizon` policy-driven ticks of every arena in one kernel launch (fs_step_n_policy).
+   P1's actions are sampled by the bf16 actor inside the tick loop, and every tick's
+   outputs land in a [horizon][N] trajectory in HBM.
+2. Features of the horizon + 1 observations, critic values, and GAE advantages, in torch on
+   the same device. The observation before tick t is the output of tick t - 1 (after a
+   same-step auto-reset that is the fresh round's state, so a terminal tick's successor is
+   never bootstrapped through: done masks it).
+3. `epochs` x `minibatches` clipped-surrogate updates of the actor and critic (fp32 torch).
+   The old log-probabilities are recomputed in fp32 from the same network, so the first
+   ratio is exactly 1.
+4. The new actor weights are copied into the rollout's device buffers (no reallocation).
+
+Nothing leaves the GPU inside an iteration, and the simulator never waits on the host.
+"""
+import time
+
+from .rollout import N_ACTIONS, N_FEATURES, FusedPolicyRollout, make_actor, obs_features
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def make_critic(hidden=64, device=None, seed=1):
+    torch = _torch()
+    g = torch.Generator().manual_seed(seed)
+    nn = torch.nn
+    net = nn.Sequential(nn.Linear(N_FEATURES, hidden), nn.Tanh(), nn.Linear(hidden, hidden), nn.Tanh(),
+                        nn.Linear(hidden, 1))
+    with torch.no_grad():
+        for p in net.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.1)
+    return net.to(device)
+
+
+def gae(rewards, values, dones, gamma, lam):
+    """Generalised advantage estimation over [T][N]: values has T + 1 rows (the last one
+    bootstraps); dones[t] = 1 cuts the recursion after tick t.  Returns (advantages, returns)."""
+    torch = _torch()
+    T = rewards.shape[0]
+    adv = torch.empty_like(rewards)
+    last = torch.zeros_like(rewards[0])
+    for t in range(T - 1, -1, -1):
+        keep = 1.0 - dones[t]
+        delta = rewards[t] + gamma * values[t + 1] * keep - values[t]
+        last = delta + gamma * lam * keep * last
+        adv[t] = last
+    return adv, adv + values[:-1]
+
+
+class PPOTrainer:
+    """PPO over a FootsiesSim (P2 = whatever the sim was created with).  `horizon` ticks per
+    rollout, all arenas in every minibatch round."""
+
+    def __init__(self, sim, actor=None, critic=None, horizon=128, gamma=0.99, lam=0.95, epochs=2, minibatches=4,
+                 lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0):
+        torch = _torch()
+        dev = sim.device
+        self.sim = sim
+        self.actor = actor if actor is not None else make_actor(device=dev, seed=seed)
+        self.critic = critic if critic is not None else make_critic(device=dev, seed=seed + 1)
+        self.rollout = FusedPolicyRollout(sim, self.actor, seed=seed)
+        self.horizon, self.gamma, self.lam = horizon, gamma, lam
+        self.epochs, self.minibatches, self.clip = epochs, minibatches, clip
+        self.vf_coef, self.ent_coef = vf_coef, ent_coef
+        self.opt = torch.optim.Adam(list(self.actor.parameters()) + list(self.critic.parameters()), lr=lr)
+        self.traj = sim.alloc_trajectory(horizon)
+        n = sim.num_envs
+        self.actions = torch.empty((horizon, n), dtype=torch.uint8, device=dev)
+        self.logp = torch.empty((horizon, n), dtype=torch.float32, device=dev)
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(seed)
+        self.stats = {}
+        # the observation before the next rollout's first tick: the sim's outputs now, then
+        # the last trajectory row (trajectory launches leave the regular outputs untouched)
+        self._next_first = None
+
+    def collect(self):
+        """One fused rollout; returns (features [T+1][N][8], actions, rewards, dones)."""
+        torch = _torch()
+        first = self._next_first if self._next_first is not None else obs_features(self.sim.outputs())
+        self.rollout.rollout(self.horizon, self.actions, self.logp, trajectory=self.traj)
+        tr = self.traj
+        T, N = self.horizon, self.sim.num_envs
+        feats = torch.empty((T + 1, N, N_FEATURES), dtype=torch.float32, device=first.device)
+        feats[0] = first
+        feats[1:] = torch.cat([tr["guard"].float() / 3.0, tr["move"].float() / 16.0, tr["move_frame"] / 55.0,
+                               tr["position"] / 4.6], dim=2)
+        self._next_first = feats[T]
+        return feats, self.actions.long(), tr["reward"].float(), tr["terminated"].float()
+
+    def update(self, feats, actions, rewards, dones):
+        torch = _torch()
+        T, N = actions.shape
+        with torch.no_grad():
+            values = self.critic(feats).squeeze(-1)  # [T+1][N]
+            adv, ret = gae(rewards, values, dones, self.gamma, self.lam)
+            x = feats[:T].reshape(T * N, N_FEATURES)
+            a = actions.reshape(T * N)
+            old = torch.log_softmax(self.actor(x), dim=1).gather(1, a[:, None])[:, 0]
+            adv = adv.reshape(T * N)
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+            ret = ret.reshape(T * N)
+        M = T * N
+        mb = (M + self.minibatches - 1) // self.minibatches
+        for _ in range(self.epochs):
+            perm = torch.randperm(M, device=x.device, generator=self.gen)
+            for i in range(0, M, mb):
+                idx = perm[i:i + mb]
+                logits = self.actor(x[idx])
+                lp_all = torch.log_softmax(logits, dim=1)
+                lp = lp_all.gather(1, a[idx, None])[:, 0]
+                ratio = torch.exp(lp - old[idx])
+                s1, s2 = ratio * adv[idx], torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv[idx]
+                pg = -torch.min(s1, s2).mean()
+                vf = (self.critic(x[idx]).squeeze(-1) - ret[idx]).pow(2).mean()
+                ent = -(lp_all.exp() * lp_all).sum(1).mean()
+                loss = pg + self.vf_coef * vf - self.ent_coef * ent
+                self.opt.zero_grad(set_to_none=True)
+                loss.backward()
+                self.opt.step()
+        self.rollout.refresh(self.actor)
+        self.stats = {"loss": loss.detach(), "policy_loss": pg.detach(), "value_loss": vf.detach(),
+                      "entropy": ent.detach(), "mean_reward": rewards.mean()}
+
+    def iterate(self):
+        self.update(*self.collect())
+
+    def train(self, iterations, sync=True):
+        """Run `iterations` PPO iterations; returns env-steps/s of the whole loop (rollout +
+        learning), timed around device synchronisation."""
+        torch = _torch()
+        torch.cuda.synchronize(self.sim.device)
+        t0 = time.perf_counter()
+        for _ in range(iterations):
+            self.iterate()
+        if sync:
+            torch.cuda.synchronize(self.sim.device)
+        return iterations * self.horizon * self.sim.num_envs / (time.perf_counter() - t0)
+
+
+__all__ = ["PPOTrainer", "make_critic", "gae", "N_ACTIONS"]

@@ -89,3 +89,24 @@ def test_fused_policy_without_outputs_and_bad_args():
         FusedPolicyRollout(d, actor).rollout(4)
     with pytest.raises(ValueError):
         FusedPolicyRollout(a, make_actor(hidden=32, device=torch.device("cuda", 0)))
+
+
+def test_ppo_iterations_learn_and_refresh_the_kernel_actor():
+    """PPOTrainer: fused rollouts + torch updates; losses finite, weights move, and the
+    kernel samples from the refreshed weights (the same seed then draws different actions)."""
+    import torch
+    from footsies_gym_amd.ppo import PPOTrainer
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(2048, p2_mode="bot", seed=5)
+    tr = PPOTrainer(sim, horizon=32, epochs=2, minibatches=4, lr=1e-2, seed=3)
+    w0 = [p.detach().clone() for p in tr.actor.parameters()]
+    k0 = [p.clone() for p in tr.rollout.params]
+    rate = tr.train(3)
+    assert rate > 0
+    for v in tr.stats.values():
+        assert bool(torch.isfinite(v))
+    assert any(not torch.equal(a, b) for a, b in zip(w0, tr.actor.parameters()))
+    for a, b in zip(tr.rollout.params, tr.actor.parameters()):
+        assert torch.equal(a, b.detach())
+    assert any(not torch.equal(a, b) for a, b in zip(k0, tr.rollout.params))
+    assert sim.steps_taken == 3 * 32
