@@ -8,6 +8,8 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -333,6 +335,47 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
   return FS_OK;
 }
 
+// The kernels address trajectory rows with 32-bit byte offsets (row t of arena a at
+// (t * N + a) * element size, up to 8 B for the f64 reward), so one launch covers at most
+// kMaxLaunchRows arena-ticks; longer fused calls run as consecutive launches over row ranges
+// of the same buffers.  Hashed actions and the actor's sampling stream are keyed by the
+// handle's step counter, which each launch advances, so the split is invisible in the results.
+constexpr uint64_t kMaxLaunchRows = 0xFFFFFFFFull / 8u;
+
+static int step_chunked(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2, uint64_t seed,
+                        const fs_outputs* traj, const fs_policy* pol) {
+  const uint64_t N = (uint64_t)h->n;
+  uint64_t rows = kMaxLaunchRows;
+  if (const char* e = getenv("FOOTSIES_MAX_LAUNCH_ROWS"))  // test hook: exercise the split at small sizes
+    rows = std::min<uint64_t>(rows, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+  const int max_n = (int)std::max<uint64_t>(1, std::min<uint64_t>(rows / N, 0x7fffffff));
+  if (n <= max_n) return step_common(h, n, p1, p2, FS_ACT_DEVICE, seed, traj, nullptr, pol);
+  for (int j = 0; j < n;) {
+    const int m = std::min(max_n, n - j);
+    const uint64_t row = (uint64_t)j * N;  // first arena-tick row of this launch
+    fs_outputs t{};
+    if (traj) {
+      t = *traj;
+      auto adv = [&](auto*& q, uint64_t per_row) { if (q) q += row * per_row; };
+      adv(t.guard, 2); adv(t.move, 2); adv(t.move_frame, 2); adv(t.position, 2); adv(t.reward, 1);
+      adv(t.terminated, 1); adv(t.truncated, 1); adv(t.frame, 1); adv(t.action, 2); adv(t.hitstun, 2);
+      adv(t.final_guard, 2); adv(t.final_move, 2); adv(t.final_move_frame, 2); adv(t.final_position, 2);
+      adv(t.final_frame, 1); adv(t.final_action, 2); adv(t.final_hitstun, 2);
+    }
+    fs_policy q{};
+    if (pol) {
+      q = *pol;
+      if (q.actions_out) q.actions_out += row;
+      if (q.logp_out) q.logp_out += row;
+    }
+    const int rc = step_common(h, m, p1 ? p1 + row : nullptr, p2 ? p2 + row : nullptr, FS_ACT_DEVICE, seed,
+                               traj ? &t : nullptr, nullptr, pol ? &q : nullptr);
+    if (rc) return rc;
+    j += m;
+  }
+  return FS_OK;
+}
+
 FS_API int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags) {
   if (!h) return FS_E_INVALID;
   if (!p1_act) return set_err(h, FS_E_INVALID, "fs_step: p1 actions required");
@@ -358,12 +401,9 @@ FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p
                      const fs_outputs* traj) {
   if (!h) return FS_E_INVALID;
   if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n: n must be > 0");
-  // the kernels index actions and trajectory rows with 32-bit offsets ([n][N][2] elements)
-  if ((uint64_t)n * (uint64_t)h->n * 2u > 0x7fffffffull)
-    return set_err(h, FS_E_INVALID, "fs_step_n: n * num_envs too large for one launch; split it");
   if ((p1_act == nullptr) != (p2_act == nullptr) && h->cfg.p2_mode == FS_P2_EXTERNAL)
     return set_err(h, FS_E_INVALID, "fs_step_n: give both action arrays or neither");
-  return step_common(h, n, p1_act, p2_act, FS_ACT_DEVICE, action_seed, traj);
+  return step_chunked(h, n, p1_act, p2_act, action_seed, traj, nullptr);
 }
 
 FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint8_t* p2_act,
@@ -372,14 +412,12 @@ FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint
   if (!pol || !pol->w1 || !pol->b1 || !pol->w2 || !pol->b2 || !pol->w3 || !pol->b3)
     return set_err(h, FS_E_INVALID, "fs_step_n_policy: all six weight arrays required");
   if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n_policy: n must be > 0");
-  if ((uint64_t)n * (uint64_t)h->n * 2u > 0x7fffffffull)
-    return set_err(h, FS_E_INVALID, "fs_step_n_policy: n * num_envs too large for one launch; split it");
   if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
     return set_err(h, FS_E_INVALID, "fs_step_n_policy: p2 actions required for FS_P2_EXTERNAL");
   if (h->cfg.frame_delay > 0)
     return set_err(h, FS_E_UNSUPPORTED, "fs_step_n_policy: the actor observes undelayed frames; frame_delay > 0 "
                                         "is not supported");
-  return step_common(h, n, nullptr, p2_act, FS_ACT_DEVICE, 0, traj, nullptr, pol);
+  return step_chunked(h, n, nullptr, p2_act, 0, traj, pol);
 }
 
 FS_API int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out) {

@@ -352,17 +352,46 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   const int a1 = e.special ? (dir ? A_B_SPECIAL : A_N_SPECIAL)
                            : (in_normal ? A_N_SPECIAL : (dir ? A_B_ATTACK : A_N_ATTACK));
   const int a2 = e.fdash ? A_DASH_FORWARD : A_DASH_BACKWARD;
-  const int a3 = (e.fwd & e.back) ? A_STAND
-                 : e.fwd          ? A_FORWARD
-                 : e.back         ? (f.prox ? A_GUARD_PROXIMITY : A_BACKWARD)
-                                  : A_STAND;
+  // movement (F:265-283) as a 4-bit table lookup on (back, forward, proximity latch)
+  constexpr uint32_t kMove = (A_STAND << 0) | (A_BACKWARD << 4) | (A_FORWARD << 8) | (A_STAND << 12) |
+                             (A_STAND << 16) | (A_GUARD_PROXIMITY << 20) | (A_FORWARD << 24) | (A_STAND << 28);
+  static_assert(A_GUARD_PROXIMITY < 16 && A_BACKWARD < 16 && A_FORWARD < 16, "movement codes are nibbles");
+  const int a3 = (int)((kMove >> (4 * ((uint32_t)e.back | ((uint32_t)e.fwd << 1) | ((uint32_t)f.prox << 2)))) & 15u);
+  const bool v1 = !early & (e.special | e.atk_down), v2 = !early & (e.fdash | e.bdash), v3 = !early;
+  if constexpr (kChainTakeIsFinal) {
+    // An attack, special or dash is set with empty take / buffer masks (tools/gen_tables.py), and
+    // the movement request comes last, so the first request that takes ends the chain: every
+    // request sees the masks of the action the fighter entered the tick with.
+    uint32_t r0 = ai_rec0(action_info(early ? a0 : 0)), r1 = ai_rec0(action_info(a1));
+    uint32_t r2 = ai_rec0(action_info(a2)), r3 = ai_rec0(action_info(a3));
+    asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));  // issued together (see below)
+    const bool t1 = v1 & (((m.take >> a1) & 1u) != 0);
+    const bool t2 = !t1 & v2 & (((m.take >> a2) & 1u) != 0);
+    const bool t3 = !t1 & !t2 & v3 & (((m.take >> a3) & 1u) != 0);
+    took = t1 | t2 | t3;
+    const bool b1 = v1 & (((m.buffer >> a1) & 1u) != 0), b2 = v2 & (((m.buffer >> a2) & 1u) != 0);
+    const bool b3 = v3 & (((m.buffer >> a3) & 1u) != 0);
+    f.act = t1 ? a1 : t2 ? a2 : t3 ? a3 : f.act;
+    f.buf = took ? NONE : b3 ? a3 : b2 ? a2 : b1 ? a1 : f.buf;
+    r = t1 ? r1 : t2 ? r2 : r3;
+    const bool set = took | early;  // SetCurrentAction ran (F:546-563)
+    f.act = early ? a0 : f.act;
+    f.frame = set ? 0 : f.frame;
+    f.hits = set ? 0 : f.hits;
+    f.rsv = set ? NONE : f.rsv;
+    f.buf = early ? NONE : f.buf;
+    f.in_back = early ? f.in_back : e.back;  // for proximity guard (F:263)
+    f.prox = early ? f.prox : false;         // F:285
+    *rec = early ? r0 : r;
+    return set;
+  }
   RInfo q0 = req_info(early ? a0 : 0), q1 = req_info(a1), q2 = req_info(a2), q3 = req_info(a3);
   // materialise all four here: left alone, the compiler sinks a read into the branch it
   // makes of a request's `take`, a second dependent LDS round trip
   asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
-  request(f, m, took, r, a1, q1, !early & (e.special | e.atk_down));
-  request(f, m, took, r, a2, q2, !early & (e.fdash | e.bdash));
-  request(f, m, took, r, a3, q3, !early);
+  request(f, m, took, r, a1, q1, v1);
+  request(f, m, took, r, a2, q2, v2);
+  request(f, m, took, r, a3, q3, v3);
   const bool set = took | early;  // SetCurrentAction ran (F:546-563)
   f.act = early ? a0 : f.act;
   f.frame = set ? 0 : f.frame;
@@ -487,9 +516,9 @@ struct BoxHits {
 template <int FM>
 __device__ __forceinline__ BoxHits box_hits(uint32_t att_info, Box4 h0, Box4 h1, float hx0, float hx1,
                                             uint32_t def_info, Box4 u0, Box4 u1, float ux0, float ux1) {
-  const int nh = (att_info >> 2) & 3, nu = def_info & 3;
-  const bool v0 = nu > 0, v1 = nu > 1;
-  // BoxBase.Overlaps (F:17-25) per pair, with each box's xMin / xMax computed once
+  // BoxBase.Overlaps (F:17-25) per pair, with each box's xMin / xMax computed once.  Absent
+  // boxes (past the record's hurt / hit count) carry an empty y-extent, yMin = +inf and
+  // yMax = -inf (tools/gen_tables.py), so their pairs fail the y-test without count checks.
   const float h0min = fsub<FM>(hx0, h0.y), h0max = fadd<FM>(hx0, h0.y);
   const float h1min = fsub<FM>(hx1, h1.y), h1max = fadd<FM>(hx1, h1.y);
   const float u0min = fsub<FM>(ux0, u0.y), u0max = fadd<FM>(ux0, u0.y);
@@ -500,8 +529,8 @@ __device__ __forceinline__ BoxHits box_hits(uint32_t att_info, Box4 h0, Box4 h1,
   BoxHits r;
   r.b0 = (att_info >> 4) & 31;
   r.b1 = (att_info >> 9) & 31;
-  r.any0 = (nh > 0) & ((v0 & ov(h0min, h0max, h0, u0min, u0max, u0)) | (v1 & ov(h0min, h0max, h0, u1min, u1max, u1)));
-  r.any1 = (nh > 1) & ((v0 & ov(h1min, h1max, h1, u0min, u0max, u0)) | (v1 & ov(h1min, h1max, h1, u1min, u1max, u1)));
+  r.any0 = ov(h0min, h0max, h0, u0min, u0max, u0) | ov(h0min, h0max, h0, u1min, u1max, u1);
+  r.any1 = ov(h1min, h1max, h1, u0min, u0max, u0) | ov(h1min, h1max, h1, u1min, u1max, u1);
   return r;
 }
 
@@ -955,6 +984,14 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
 // outputs (FE:336-380, 537-549): each lane writes its own column of the [N][2]
 // pairs (one byte / float per lane, fully coalesced); lane k = 0 the per-arena ones
 // ---------------------------------------------------------------------------
+// Stores at a 32-bit byte offset from a kernel-argument base: the address is one SGPR pair plus
+// one VGPR (global_store ... saddr), with no 64-bit address arithmetic per store.  The host
+// splits launches so every trajectory offset fits (fs_api.cpp, kMaxLaunchRows).
+template <class T>
+__device__ __forceinline__ void st_off(T* base, uint32_t byte_off, T v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = v;
+}
+
 __device__ __forceinline__ void write_obs(const Lane& L, uint8_t* guard, uint8_t* move, float* move_frame,
                                           float* position, int32_t* frame, uint8_t* action, uint8_t* hitstun,
                                           uint32_t r) {
@@ -962,13 +999,13 @@ __device__ __forceinline__ void write_obs(const Lane& L, uint8_t* guard, uint8_t
   if (a == A_DEAD || a == A_WIN) a = A_STAND;  // FE:537-549
   const int mf = (a == A_STAND || a == A_FORWARD || a == A_BACKWARD) ? 0 : L.f.frame;  // FE:339-358
   const uint32_t c = 2 * r + L.k;
-  guard[c] = (uint8_t)L.f.guard;
-  move[c] = (uint8_t)a;
-  move_frame[c] = (float)mf;
-  position[c] = L.f.x;
-  action[c] = L.rec_count > 0 ? (uint8_t)L.rec : 0;
-  hitstun[c] = (uint8_t)L.f.stun;
-  frame[r] = L.frame_count;  // both lanes hold the replica: the same value to the same address
+  st_off(guard, c, (uint8_t)L.f.guard);
+  st_off(move, c, (uint8_t)a);
+  st_off(move_frame, 4 * c, (float)mf);
+  st_off(position, 4 * c, L.f.x);
+  st_off(action, c, L.rec_count > 0 ? (uint8_t)L.rec : (uint8_t)0);
+  st_off(hitstun, c, (uint8_t)L.f.stun);
+  st_off(frame, 4 * r, (int32_t)L.frame_count);  // both lanes hold the replica: the same value to the same address
 }
 
 __device__ __forceinline__ void write_main(const Lane& L, const DevOutputs& o, uint32_t r) {
@@ -1013,9 +1050,9 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.ai = action_info(L.f.act);
     settle(next);
     write_main(L, o, r);
-    o.reward[r] = 0.0;  // per-arena outputs: both lanes store the same value (no divergent branch)
-    o.terminated[r] = 0;
-    o.truncated[r] = 0;
+    st_off(o.reward, 8 * r, 0.0);  // per-arena outputs: both lanes store the same value (no divergent branch)
+    st_off(o.terminated, r, (uint8_t)0);
+    st_off(o.truncated, r, (uint8_t)0);
     return;
   }
   // the actor inputs of this frame (TrainingManager.p1Input/p2Input, BC:383-447)
@@ -1094,9 +1131,9 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   }
   L.ai = action_info(L.f.act);  // for the next tick (hits and resets set actions too)
   write_main(L, o, r);
-  o.reward[r] = reward;  // identical on both lanes of the arena
-  o.terminated[r] = over ? 1 : 0;
-  o.truncated[r] = 0;
+  st_off(o.reward, 8 * r, reward);  // identical on both lanes of the arena
+  st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
+  st_off(o.truncated, r, (uint8_t)0);
 }
 
 // P1's observation features for the in-kernel actor (fs_policy.h), packed bf16x2:

@@ -204,7 +204,10 @@ int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, co
  * [n][N][2]) receiving every tick's outputs; traj == NULL writes each tick
  * into the handle's regular outputs (the last tick remains visible; with
  * frame_delay > 0 the n ticks are then launched one by one, since the delayed
- * queue consumes every tick's row). */
+ * queue consumes every tick's row).  Trajectory rows are addressed with 32-bit
+ * byte offsets, so a call with n * N above 2^29 - 1 arena-ticks runs as several
+ * consecutive launches over row ranges of the same buffers, with identical
+ * results. */
 int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act,
               uint64_t action_seed, const fs_outputs* traj);
 

@@ -442,3 +442,43 @@ def test_native_consumer_under_host_sanitizers():
     r = subprocess.run([os.path.join(d, "abi_lockstep")], env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "all checks passed" in r.stdout
+
+
+@pytest.mark.parametrize("p2", ["external", "bot"])
+def test_long_fused_launches_split_like_one(monkeypatch, p2):
+    """A fused call longer than one launch's 32-bit trajectory offsets allow runs as several
+    launches over row ranges of the same buffers (fs_api.cpp step_chunked).  With the split
+    forced at 3 ticks per launch, trajectories, actor samples and final states equal those of
+    single launches: device actions, hashed actions and the in-kernel actor."""
+    import torch
+    from footsies_gym_amd.rollout import FusedPolicyRollout, make_actor
+    from footsies_gym_amd.simulator import FootsiesSim
+    N, T = 256, 37
+    mk = lambda: FootsiesSim(N, p2_mode=p2, seed=11)  # noqa: E731
+    one, split = mk(), mk()
+    p1, q2 = one.hash_actions(T, seed=5, p2=(p2 == "external"))
+    runs = []
+    for sim, rows in ((one, None), (split, "1000")):
+        if rows:
+            monkeypatch.setenv("FOOTSIES_MAX_LAUNCH_ROWS", rows)
+        got = []
+        tr = sim.alloc_trajectory(T)
+        sim.step_n(T, p1, q2, trajectory=tr)                  # device actions
+        got.append(tr)
+        if p2 == "bot":
+            tr = sim.alloc_trajectory(T)
+            sim.step_n(T, None, None, action_seed=9, trajectory=tr)  # hashed actions
+            got.append(tr)
+            ro = FusedPolicyRollout(sim, make_actor(device=sim.device, seed=2), seed=4)
+            tr = sim.alloc_trajectory(T)
+            acts, logp = ro.rollout(T, trajectory=tr)         # actor in the loop
+            got += [tr, {"actions": acts, "logp": logp}]
+        torch.cuda.synchronize()
+        runs.append((got, sim.get_state()))
+        monkeypatch.delenv("FOOTSIES_MAX_LAUNCH_ROWS", raising=False)
+    for a, b in zip(runs[0][0], runs[1][0]):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    compare_states(runs[0][1], runs[1][1])
+    one.close()
+    split.close()
