@@ -199,6 +199,32 @@ def pmc_traffic(kernel, envs, ticks):
     return best
 
 
+def issue_profile(kernel, envs, ticks):
+    """The step kernel's instruction-issue picture from the committed SQ counter summary
+    (profiles/*_sq.json, tools/pmc_table.py --json over tools/prof_pmc.sh passes of the same
+    kernel at the same arena count): instructions issued per wave-tick, wave cycles per
+    wave-tick (quad-cycles) and their quotient, the fraction of one wave's issue ceiling (one
+    instruction per 4 cycles, MI355X_MICROARCH.md constants table) that the kernel sustains.
+    Reported beside the HBM roofline: this kernel is bound by its instruction stream, not by
+    bytes.  None when no summary matches."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))):
+        with open(path) as f:
+            doc = json.load(f)
+        for k in doc.get("kernels", []):
+            if k["kernel"] == kernel and k["envs"] == envs:
+                pw = k["per_wave_tick"]
+                best = {"bound": "wave instruction issue (1 instruction / 4 cycles / wave)",
+                        "insts_per_wave_tick": round(k["insts_per_wave_tick"], 1),
+                        "valu_per_wave_tick": round(pw.get("SQ_INSTS_VALU", 0.0), 1),
+                        "salu_per_wave_tick": round(pw.get("SQ_INSTS_SALU", 0.0), 1),
+                        "wave_quad_cycles_per_wave_tick": round(pw.get("SQ_WAVE_CYCLES", 0.0), 1),
+                        "frac": k["wave_issue_frac"], "ticks_per_launch_profiled": k["ticks_per_launch"],
+                        "source": os.path.relpath(path, ROOT)}
+    return best
+
+
 def main():
     args = parse()
     import torch
@@ -360,7 +386,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": tr[0] if tr else None,
                      "traffic_source": tr[1] if tr else None,
                      "kernel": kname, "avg_launch_us": kt * 1e6, "median_launch_us": kmed * 1e6,
-                     "algorithmic_bytes_per_launch": bytes_per_launch},
+                     "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "issue": issue_profile(kname, N, ticks)},
         other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
         "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
                                    "note": "fs_step with FS_ACT_HOST (PCIe-inclusive action hand-over)"},

@@ -1,13 +1,14 @@
 #!/bin/bash
 # PMC passes for the step kernel (one counter group per rocprofv3 run; no trace domains
-# combined with --pmc).  Usage (on the GPU box, from the repo root): tools/prof_pmc.sh OUTDIR MODE
+# combined with --pmc).  Usage (on the GPU box, from the repo root):
+#   tools/prof_pmc.sh OUTDIR MODE [profile_driver args...]
 set -e
-OUT=${1:-gpurun_out/pmc}; MODE=${2:-fused}
+OUT=${1:-gpurun_out/pmc}; MODE=${2:-fused}; shift 2 || true; DARGS="$@"
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp; export TMPDIR=/tmp
 run() { name=$1; shift
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/$name" -o run "$@" -- python3 "$ROOT/tools/profile_driver.py" --mode $MODE > "$ROOT/$OUT/$name.log" 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/$name" -o run "$@" -- python3 "$ROOT/tools/profile_driver.py" --mode $MODE $DARGS > "$ROOT/$OUT/$name.log" 2>&1
 }
 run trace
 run fetch --pmc FETCH_SIZE
