@@ -38,18 +38,74 @@ def make_critic(hidden=64, device=None, seed=1):
     return net.to(device)
 
 
+_WGRAD_CHUNK = 8192
+
+
+def _weight_grad(g, x):
+    """g^T x for tall, skinny g [M, out] and x [M, in] (M ~ 2M samples, out/in <= 64): one
+    batched GEMM over row chunks, then a sum over the chunks.  A single GEMM with a reduction
+    dimension of millions and a 64 x 64 result leaves hipBLASLt a handful of output tiles to
+    split; the batched form runs ~13x faster on MI355X (fp32, 2.1M x 64: 0.2 ms vs 2.6 ms)."""
+    torch = _torch()
+    M = g.shape[0]
+    full = (M // _WGRAD_CHUNK) * _WGRAD_CHUNK
+    out = torch.zeros((g.shape[1], x.shape[1]), dtype=g.dtype, device=g.device)
+    if full:
+        gc = g[:full].reshape(-1, _WGRAD_CHUNK, g.shape[1])
+        xc = x[:full].reshape(-1, _WGRAD_CHUNK, x.shape[1])
+        out += torch.bmm(gc.transpose(1, 2), xc).sum(0)
+    if full < M:
+        out += g[full:].t() @ x[full:]
+    return out
+
+
+def _linear_fn():
+    torch = _torch()
+
+    class SkinnyLinear(torch.autograd.Function):
+        """y = x W^T + b with the weight gradient formed by `_weight_grad`."""
+
+        @staticmethod
+        def forward(ctx, x, w, b):
+            ctx.save_for_backward(x, w)
+            return torch.addmm(b, x, w.t())
+
+        @staticmethod
+        def backward(ctx, gy):
+            x, w = ctx.saved_tensors
+            gy = gy.contiguous()
+            return gy @ w, _weight_grad(gy, x.contiguous()), gy.sum(0)
+
+    return SkinnyLinear
+
+
+_SKINNY = None
+
+
+def mlp(net, x):
+    """net(x) for an nn.Sequential of Linear / activation layers, with every Linear through
+    SkinnyLinear (same values; the weight gradients take the batched path)."""
+    global _SKINNY
+    torch = _torch()
+    if _SKINNY is None:
+        _SKINNY = _linear_fn()
+    for m in net:
+        x = _SKINNY.apply(x, m.weight, m.bias) if isinstance(m, torch.nn.Linear) else m(x)
+    return x
+
+
 def gae(rewards, values, dones, gamma, lam):
     """Generalised advantage estimation over [T][N]: values has T + 1 rows (the last one
     bootstraps); dones[t] = 1 cuts the recursion after tick t.  Returns (advantages, returns)."""
     torch = _torch()
     T = rewards.shape[0]
+    keep = 1.0 - dones
+    delta = rewards + gamma * values[1:] * keep - values[:-1]  # every tick's TD error at once
+    coef = (gamma * lam) * keep
     adv = torch.empty_like(rewards)
-    last = torch.zeros_like(rewards[0])
-    for t in range(T - 1, -1, -1):
-        keep = 1.0 - dones[t]
-        delta = rewards[t] + gamma * values[t + 1] * keep - values[t]
-        last = delta + gamma * lam * keep * last
-        adv[t] = last
+    adv[T - 1] = delta[T - 1]
+    for t in range(T - 2, -1, -1):  # the backward recursion: one fused multiply-add per tick
+        torch.addcmul(delta[t], coef[t], adv[t + 1], out=adv[t])
     return adv, adv + values[:-1]
 
 
@@ -112,13 +168,13 @@ class PPOTrainer:
             perm = torch.randperm(M, device=x.device, generator=self.gen)
             for i in range(0, M, mb):
                 idx = perm[i:i + mb]
-                logits = self.actor(x[idx])
+                logits = mlp(self.actor, x[idx])
                 lp_all = torch.log_softmax(logits, dim=1)
                 lp = lp_all.gather(1, a[idx, None])[:, 0]
                 ratio = torch.exp(lp - old[idx])
                 s1, s2 = ratio * adv[idx], torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv[idx]
                 pg = -torch.min(s1, s2).mean()
-                vf = (self.critic(x[idx]).squeeze(-1) - ret[idx]).pow(2).mean()
+                vf = (mlp(self.critic, x[idx]).squeeze(-1) - ret[idx]).pow(2).mean()
                 ent = -(lp_all.exp() * lp_all).sum(1).mean()
                 loss = pg + self.vf_coef * vf - self.ent_coef * ent
                 self.opt.zero_grad(set_to_none=True)
