@@ -419,6 +419,15 @@ __device__ __forceinline__ void update_movement(Fighter& f, float walk_fwd, floa
   f.x = (f.stun <= 0 && v != 0.0f) ? nx : f.x;
 }
 
+// Frame record `rec` of facing `k` in LDS.  The byte offset is formed with 24-bit multiplies
+// (v_mul_u32_u24, full rate): indexing sT.recs[k][rec] directly makes a 64-bit v_mad_u64_u32
+// and a v_mul_lo_u32, both quarter-rate, on the dependency chain of every tick.
+__device__ __forceinline__ const FrameRec& frame_rec(uint32_t k, uint32_t rec) {
+  const char* base = reinterpret_cast<const char*>(&sT.recs[0][0]);
+  return *reinterpret_cast<const FrameRec*>(base + __umul24(k, (uint32_t)sizeof(sT.recs[0])) +
+                                            __umul24(rec, (uint32_t)sizeof(FrameRec)));
+}
+
 // the frame record of (act, frame)
 __device__ __forceinline__ int frame_record(const Fighter& f) {
   return sT.rec_index[f.act * kFrameStride + min(f.frame, kFrameStride - 1)];
@@ -1075,11 +1084,12 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   uint32_t rec_set;
   const bool set = update_action_request(L.f, e, ai, &rec_set);
   L.f.rec = set ? (int)rec_set : rec_cont;
-  const FrameRec& R = sT.recs[k][L.f.rec];
+  const FrameRec& R = frame_rec(k, (uint32_t)L.f.rec);
   // the collision's boxes: mine and the partner's (its record index crosses the pair now)
   const int o_rec = xpair(L.f.rec);
   const Box4 my_hurt0 = box4(R.hurt[0]), my_hurt1 = box4(R.hurt[1]);
-  const Box4 their_hit0 = box4(sT.recs[0][o_rec].hit[0]), their_hit1 = box4(sT.recs[0][o_rec].hit[1]);
+  const FrameRec& O = frame_rec(0, (uint32_t)o_rec);
+  const Box4 their_hit0 = box4(O.hit[0]), their_hit1 = box4(O.hit[1]);
   update_movement<FM>(L.f, walk_fwd, walk_back, R.vel);
   update_boxes<FM>(L.f, R);
   push_character_vs_character<FM>(L.f, k);
@@ -1129,11 +1139,11 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     }
     L.has_term = false;
   }
-  L.ai = action_info(L.f.act);  // for the next tick (hits and resets set actions too)
   write_main(L, o, r);
   st_off(o.reward, 8 * r, reward);  // identical on both lanes of the arena
   st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
   st_off(o.truncated, r, (uint8_t)0);
+  L.ai = action_info(L.f.act);  // for the next tick (hits and resets set actions too)
 }
 
 // P1's observation features for the in-kernel actor (fs_policy.h), packed bf16x2:
