@@ -643,18 +643,18 @@ __device__ __forceinline__ bool attack_forced(uint32_t b, uint32_t opp) {
 // one draw descriptor per bucket, plan lengths.
 struct alignas(16) BotDraw {
   uint32_t map;    // nibble r = the plan drawn for r
-  uint32_t magic;  // ceil(2^32 / n): r = v - n * umulhi(v, magic) is exact for v < 2^20
+  uint32_t magic;  // ceil(2^23 / n) (< 2^23): floor(v n^-1) = (v magic) >> 23 for v < 2^20, n < 8
   uint32_t n;
   uint32_t c16;    // 65536 % n
 };
 struct alignas(16) BotTables {
   BotDraw move[5], attack[5];
-  uint32_t move_codes[7][6];  // plan p, index i: input bits at 2 (i & 15) of word i >> 4
+  uint32_t move_codes[7][8];  // plan p, index i: input bits at 2 (i & 15) of word i >> 4 (rows padded to 32 B)
   uint8_t move_len[8], attack_len[8], attack_hold[8];
   uint32_t pad[2];
 };
 constexpr BotDraw make_draw(uint32_t n, uint32_t map) {
-  return BotDraw{map, (uint32_t)((0x100000000ull + n - 1) / n), n, 65536u % n};
+  return BotDraw{map, (uint32_t)(((1u << 23) + n - 1) / n), n, 65536u % n};
 }
 constexpr BotTables make_bot_tables() {
   BotTables t{};
@@ -707,10 +707,15 @@ __device__ __forceinline__ void stage_tables() {
 }
 
 // Random.Range(0, n) = x % n for the draw descriptor: x = h 2^16 + l, so x % n = (h (2^16 % n) + l) % n
-// with the inner value < 2^20, where the magic multiply is exact
+// with the inner value v < 2^19.  The quotient is (v magic) >> 23 with magic = ceil(2^23 / n): the
+// product exceeds v / n by less than v / 2^23 < 1/8 < 1/n, which cannot carry past the next
+// integer.  Every factor is below 2^24, so the product is two full-rate 24-bit multiplies
+// (v_mul_u32_u24 / v_mul_hi_u32_u24, bits 31:0 and 47:32) instead of the quarter-rate 32-bit ones.
 __device__ __forceinline__ uint32_t draw_mod(uint32_t x, const BotDraw& d) {
-  const uint32_t v = (x >> 16) * d.c16 + (x & 0xFFFFu);
-  return v - d.n * __umulhi(v, d.magic);
+  const uint32_t v = __umul24(x >> 16, d.c16) + (x & 0xFFFFu);
+  const uint64_t prod = (uint64_t)(v & 0xFFFFFFu) * (uint64_t)(d.magic & 0xFFFFFFu);  // 24 x 24 bits
+  const uint32_t q = (uint32_t)(prod >> 23);
+  return v - __umul24(d.n, q);
 }
 
 // getNextAIInput (AI:41-66) for the P2 bot.  The ascending copy loop of
@@ -740,7 +745,7 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, float dist, uint32_t 
   const bool mbusy = b.mplan != 0, abusy = b.aplan != 0;
   const uint32_t mp = mbusy ? b.mplan - 1 : 0u, ap = abusy ? b.aplan - 1 : 0u;
   const uint32_t mi = b.midx, ai = b.aidx;
-  const uint32_t in_m = (sBot.move_codes[mp][mi >> 4] >> (2 * (mi & 15))) & 3u;
+  const uint32_t in_m = (sBot.move_codes[mp][mi >> 4] >> (2 * (mi & 15))) & 3u;  // 32-B rows: a shift, not a multiply
   const bool press = (ai < sBot.attack_hold[ap]) | ((ap == AP_TWO_HIT) & (ai == 4));
   const uint32_t input = (mbusy ? in_m : 0u) | ((abusy & press) ? IN_ATTACK : 0u);
   const bool forced = attack_forced(bucket, opp);
@@ -773,7 +778,7 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, float dist, uint32_t 
 // control flow that is uniform across a pair, so the partner lane is active.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t xpair(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1 /* quad_perm(1,0,3,2) */, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1 /* quad_perm(1,0,3,2) */, 0xF, 0xF, true);
 }
 __device__ __forceinline__ int xpair(int v) { return (int)xpair((uint32_t)v); }
 __device__ __forceinline__ float xpair(float v) { return __uint_as_float(xpair(__float_as_uint(v))); }
