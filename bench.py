@@ -36,7 +36,9 @@ STEP_IO_BYTES = 40      # per env-step: 2 B actions in + 38 B outputs out (inclu
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
+    # 10 000 timed ticks = 10 fused launches: SURVEY 8(d)'s C3 protocol (5 runs of 2 000 steps)
+    # as one timed region, so the fixed host cost of the first launch is amortised the same way
+    ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="arenas per GPU (weak scaling)")
     ap.add_argument("--global-envs", type=int, default=0,

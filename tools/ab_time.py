@@ -39,9 +39,24 @@ for mode in ("external", "bot"):
     torch.cuda.synchronize()
     d = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
     res.append(d[len(d) // 2])
+    if mode == "external":  # the host-driven path: fs_step, one launch per tick (VectorEnv.step)
+        def one(k):
+            check(lib().fs_step(sim.handle, C.c_void_p(p1.data_ptr() + k * N), q2 if q2 is None else
+                                C.c_void_p(p2.data_ptr() + k * N), _abi.FS_ACT_DEVICE), sim.handle)
+        for k in range(20):
+            one(k)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(2e7))
+        e0.record()
+        for k in range(300):
+            one(k)
+        e1.record()
+        torch.cuda.synchronize()
+        step_us = e0.elapsed_time(e1) * 1e3 / 300
     del traj, p1, p2
     sim.close()
-print("RESULT %%.1f %%.1f" %% tuple(res))
+print("RESULT %%.1f %%.1f %%.2f" %% (res[0], res[1], step_us))
 '''
 
 
@@ -63,18 +78,19 @@ def main():
             if p.returncode or not line:
                 print("%s: error\n%s" % (lib, p.stderr[-800:]), flush=True)
                 sys.exit(1)
-            ext, bot = (float(x) for x in line[0].split()[1:])
-            times[lib].append((ext, bot))
-            print("round %d %-40s C3 %8.1f us  C2 %8.1f us" % (r, lib, ext, bot), flush=True)
+            ext, bot, step = (float(x) for x in line[0].split()[1:])
+            times[lib].append((ext, bot, step))
+            print("round %d %-40s C3 %8.1f us  C2 %8.1f us  fs_step %6.2f us" % (r, lib, ext, bot, step), flush=True)
     base = None
     for lib, ts in times.items():
         ext = sorted(t[0] for t in ts)[len(ts) // 2]
         bot = sorted(t[1] for t in ts)[len(ts) // 2]
+        step = sorted(t[2] for t in ts)[len(ts) // 2]
         if base is None:
-            base = (ext, bot)
-        print("%-40s C3 %8.1f us (%.3e env-steps/s, %+.1f%%)  C2 %8.1f us (%.3e, %+.1f%%)" % (
+            base = (ext, bot, step)
+        print("%-40s C3 %8.1f us (%.3e env-steps/s, %+.1f%%)  C2 %8.1f us (%.3e, %+.1f%%)  fs_step %.2f us (%+.1f%%)" % (
             lib, ext, a.envs * a.ticks / ext * 1e6, 100 * (base[0] / ext - 1), bot, a.envs * a.ticks / bot * 1e6,
-            100 * (base[1] / bot - 1)), flush=True)
+            100 * (base[1] / bot - 1), step, 100 * (base[2] / step - 1)), flush=True)
 
 
 if __name__ == "__main__":
