@@ -7,13 +7,13 @@
 //
 //   load (coalesced 4/8/16-B per lane) -> n ticks in registers -> store
 //
-// Frame data is one ~6 KB image staged into LDS per block: per action a 16-B
-// ActionInfo (frame count, loop, cancel window), and per (action, frame) an
-// index into 51 de-duplicated 96-B frame records holding every box's geometry,
-// the velocity and the hitbox attack bits -- the window scans of
-// ActionData.cs:87-168 resolved offline (tools/gen_tables.py).  A tick needs
-// four dependent LDS round trips: action info, requested actions' infos, record
-// index, record.  The 180-deep input histories (Fighter.cs:98-101) are two 16-frame
+// Frame data is one ~21 KB image staged into LDS per block: per action a 16-B
+// ActionInfo (frame count, loop, cancel window), per (action, frame) an index into
+// 51 de-duplicated 96-B frame records holding every box's geometry, the velocity and
+// the hitbox attack bits -- the window scans of ActionData.cs:87-168 resolved offline
+// (tools/gen_tables.py) -- and the request chain's outcome per (action, window state,
+// inputs).  A tick's dependent LDS round trips: action info, then the record index and
+// the request-table entry together, then the record.  The 180-deep input histories (Fighter.cs:98-101) are two 16-frame
 // shift registers (backward / forward relative to the fighter's facing) plus a
 // saturating attack-hold counter: the reference
 // only reads input[0..16] for dashes (Fighter.cs:585-635, dashAllowFrame 9) and
@@ -324,10 +324,9 @@ __device__ __forceinline__ void request(Fighter& f, ReqMasks& m, bool& took, uin
   took |= take;
 }
 
-// UpdateActionRequest (F:201-286).  Every request target is decided from the inputs and the
-// state before the first request, so the four ReqInfo reads are issued together; the chain
-// is branch-free.  Returns whether SetCurrentAction ran; then *rec is the new action's
-// frame-0 record.
+// UpdateActionRequest (F:201-286): hasWon's RequestAction(WIN), the reserved / buffered early
+// returns, then the request chain as one table read; branch-free apart from the hasWon skip.
+// Returns whether SetCurrentAction ran; then *rec is the new action's frame-0 record.
 __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEval& e, AInfo ai, uint32_t* rec) {
   ReqMasks m = req_masks(f, ai);
   bool took = false;
@@ -346,61 +345,32 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   const bool take_buf = !take_rsv && buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0;
   const bool early = take_rsv | take_buf;
   const int a0 = take_rsv ? rsv : buf;
-  // special / attack (F:234-254), dash (F:256-259), movement (F:265-283)
-  const bool dir = e.fwd | e.back;
-  const bool in_normal = (f.act == A_N_ATTACK || f.act == A_B_ATTACK) && f.frame < ai_frame_count(ai);
-  const int a1 = e.special ? (dir ? A_B_SPECIAL : A_N_SPECIAL)
-                           : (in_normal ? A_N_SPECIAL : (dir ? A_B_ATTACK : A_N_ATTACK));
-  const int a2 = e.fdash ? A_DASH_FORWARD : A_DASH_BACKWARD;
-  // movement (F:265-283) as a 4-bit table lookup on (back, forward, proximity latch)
-  constexpr uint32_t kMove = (A_STAND << 0) | (A_BACKWARD << 4) | (A_FORWARD << 8) | (A_STAND << 12) |
-                             (A_STAND << 16) | (A_GUARD_PROXIMITY << 20) | (A_FORWARD << 24) | (A_STAND << 28);
-  static_assert(A_GUARD_PROXIMITY < 16 && A_BACKWARD < 16 && A_FORWARD < 16, "movement codes are nibbles");
-  const int a3 = (int)((kMove >> (4 * ((uint32_t)e.back | ((uint32_t)e.fwd << 1) | ((uint32_t)f.prox << 2)))) & 15u);
-  const bool v1 = !early & (e.special | e.atk_down), v2 = !early & (e.fdash | e.bdash), v3 = !early;
-  if constexpr (kChainTakeIsFinal) {
-    // An attack, special or dash is set with empty take / buffer masks (tools/gen_tables.py), and
-    // the movement request comes last, so the first request that takes ends the chain: every
-    // request sees the masks of the action the fighter entered the tick with.
-    uint32_t r0 = ai_rec0(action_info(early ? a0 : 0)), r1 = ai_rec0(action_info(a1));
-    uint32_t r2 = ai_rec0(action_info(a2)), r3 = ai_rec0(action_info(a3));
-    asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));  // issued together (see below)
-    const bool t1 = v1 & (((m.take >> a1) & 1u) != 0);
-    const bool t2 = !t1 & v2 & (((m.take >> a2) & 1u) != 0);
-    const bool t3 = !t1 & !t2 & v3 & (((m.take >> a3) & 1u) != 0);
-    took = t1 | t2 | t3;
-    const bool b1 = v1 & (((m.buffer >> a1) & 1u) != 0), b2 = v2 & (((m.buffer >> a2) & 1u) != 0);
-    const bool b3 = v3 & (((m.buffer >> a3) & 1u) != 0);
-    f.act = t1 ? a1 : t2 ? a2 : t3 ? a3 : f.act;
-    f.buf = took ? NONE : b3 ? a3 : b2 ? a2 : b1 ? a1 : f.buf;
-    r = t1 ? r1 : t2 ? r2 : r3;
-    const bool set = took | early;  // SetCurrentAction ran (F:546-563)
-    f.act = early ? a0 : f.act;
-    f.frame = set ? 0 : f.frame;
-    f.hits = set ? 0 : f.hits;
-    f.rsv = set ? NONE : f.rsv;
-    f.buf = early ? NONE : f.buf;
-    f.in_back = early ? f.in_back : e.back;  // for proximity guard (F:263)
-    f.prox = early ? f.prox : false;         // F:285
-    *rec = early ? r0 : r;
-    return set;
-  }
-  RInfo q0 = req_info(early ? a0 : 0), q1 = req_info(a1), q2 = req_info(a2), q3 = req_info(a3);
-  // materialise all four here: left alone, the compiler sinks a read into the branch it
-  // makes of a request's `take`, a second dependent LDS round trip
-  asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
-  request(f, m, took, r, a1, q1, v1);
-  request(f, m, took, r, a2, q2, v2);
-  request(f, m, took, r, a3, q3, v3);
+  // The request chain (special / attack F:234-254, dash F:256-259, movement F:265-283, each
+  // through RequestAction F:472-510) as one read of kTables.req_table: its outcome depends only
+  // on the action, whether it has ended or sits in its cancel window, the attack / dash / held
+  // direction inputs and the proximity latch (tools/gen_tables.py runs the chain for each).
+  const bool ended = f.frame >= ai_frame_count(ai);
+  const bool inwin = (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai));
+  const uint32_t cls = ended ? 2u : (inwin ? 1u : 0u);
+  const uint32_t atk = e.special ? 1u : (e.atk_down ? 2u : 0u);
+  const uint32_t dash = e.fdash ? 1u : (e.bdash ? 2u : 0u);
+  const uint32_t held = (uint32_t)e.back | ((uint32_t)e.fwd << 1);
+  const uint32_t idx =
+      (((__umul24((uint32_t)f.act, 27u) + __umul24(cls, 9u) + 3u * atk + dash) << 3) | (held << 1)) | (uint32_t)f.prox;
+  uint32_t q = sT.req_table[idx];
+  uint32_t r0 = ai_rec0(action_info(early ? a0 : 0));
+  asm volatile("" : "+v"(q), "+v"(r0));  // both reads in flight together
+  took = !early & (((q >> 11) & 1u) != 0);
+  const bool bset = !early & (((q >> 10) & 1u) != 0);
   const bool set = took | early;  // SetCurrentAction ran (F:546-563)
-  f.act = early ? a0 : f.act;
+  f.act = early ? a0 : (took ? (int)(q & 31u) : f.act);
+  f.buf = set ? NONE : (bset ? (int)((q >> 5) & 31u) : f.buf);
   f.frame = set ? 0 : f.frame;
   f.hits = set ? 0 : f.hits;
   f.rsv = set ? NONE : f.rsv;
-  f.buf = early ? NONE : f.buf;
   f.in_back = early ? f.in_back : e.back;  // for proximity guard (F:263)
   f.prox = early ? f.prox : false;         // F:285
-  *rec = early ? q0.z : r;
+  *rec = early ? r0 : ((q >> 12) & 255u);
   return set;
 }
 
