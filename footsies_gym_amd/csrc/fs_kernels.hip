@@ -355,8 +355,7 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   const uint32_t atk = e.special ? 1u : (e.atk_down ? 2u : 0u);
   const uint32_t dash = e.fdash ? 1u : (e.bdash ? 2u : 0u);
   const uint32_t held = (uint32_t)e.back | ((uint32_t)e.fwd << 1);
-  const uint32_t idx =
-      (((__umul24((uint32_t)f.act, 27u) + __umul24(cls, 9u) + 3u * atk + dash) << 3) | (held << 1)) | (uint32_t)f.prox;
+  const uint32_t idx = ((uint32_t)f.act << 8) | ((9u * cls + 3u * atk + dash) << 3) | (held << 1) | (uint32_t)f.prox;
   uint32_t q = sT.req_table[idx];
   uint32_t r0 = ai_rec0(action_info(early ? a0 : 0));
   asm volatile("" : "+v"(q), "+v"(r0));  // both reads in flight together
