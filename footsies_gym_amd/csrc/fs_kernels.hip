@@ -860,7 +860,7 @@ template <int FM>
 __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, Box4 my_hurt0, Box4 my_hurt1,
                                                          Box4 their_hit0, Box4 their_hit1) {
   const uint32_t o_info = xpair(f.info);
-  if ((((f.info | o_info) >> 2) & 3) == 0) return;  // only attack actions carry hitboxes
+  // (no wave-level skip: absent hitboxes have empty y-extents and never overlap)
   const int o_hits = xpair(f.hits);
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
   const BoxHits bh = box_hits<FM>(o_info, their_hit0, their_hit1, o_hx0, o_hx1, f.info, my_hurt0, my_hurt1,
