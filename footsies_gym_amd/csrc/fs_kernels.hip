@@ -187,8 +187,12 @@ __device__ __forceinline__ float bb_xmax(float x, float w) {
 // ---------------------------------------------------------------------------
 // input (F:172-188, 569-666)
 // ---------------------------------------------------------------------------
+// The inputs UpdateActionRequest reads, as small integer codes (the request table's index
+// fields) computed with bit arithmetic in VGPRs rather than as compare-and-select booleans.
 struct InputEval {
-  bool fwd, back, special, atk_down, fdash, bdash;
+  uint32_t held;  // bit 0 = backward held on input[0], bit 1 = forward (facing-relative)
+  uint32_t atk;   // 1 = special (attack released after the charge), 2 = attack pressed, else 0
+  uint32_t dash;  // 1 = forward dash, 2 = backward dash, else 0
 };
 
 // Left/Right -> (bit0 = backward, bit1 = forward).  P1 faces right, P2 left for
@@ -230,26 +234,26 @@ __device__ __forceinline__ InputEval update_input(Fighter& f, uint32_t in, int k
   const uint32_t old_hist = f.hist;
   const int old_hold = f.hold;
   const uint32_t r0 = rel_bits(in, k);
-  const uint32_t r1 = (old_hist & 1) | ((old_hist >> 15) & 2);  // input[1] after the shift, relative
   f.hist = ((old_hist << 1) & 0xFFFEFFFEu) | (r0 & 1) | ((r0 & 2) << 15);
   f.hold = (in & IN_ATTACK) ? min(old_hold + 1, 63) : 0;
-  const bool in1_atk = old_hold > 0;
   InputEval e;
-  e.fwd = r0 & 2;
-  e.back = r0 & 1;
-  e.atk_down = (in & IN_ATTACK) && !in1_atk;                            // inputDown[0] & Attack
-  e.special = !(in & IN_ATTACK) && old_hold >= kSpecialHoldFrame - 1;  // inputUp[0] & Attack, input[1..59] held
-  // dash parsers over input[1..16] (bit j-1 of each mask = input[j])
+  e.held = r0;
+  // inputDown[0] & Attack with input[1] released; inputUp[0] & Attack after input[1..59] held
+  const uint32_t atk_now = (in >> 2) & 1u;
+  const uint32_t held_long = ((uint32_t)(old_hold - (kSpecialHoldFrame - 1)) >> 31) ^ 1u;  // old_hold >= 59
+  const uint32_t was_up = (uint32_t)(old_hold - 1) >> 31;                                  // old_hold == 0
+  e.atk = (held_long & ~atk_now & 1u) | ((atk_now & was_up) << 1);
+  // dash parsers over input[1..16] (bit j-1 of each mask = input[j]): j = the first input among
+  // input[1..8] with a direction (8 when none); masking F and B to that window makes isF = isB = 0
+  // when there is none, so no separate "found" test is needed
   const uint32_t B = old_hist & 0xFFFFu, F = old_hist >> 16, E = B | F;
   const uint32_t win = (1u << (kDashAllowFrame - 1)) - 1u;
-  const uint32_t e8 = E & win;
-  // branch-free: j = first i - 1 in 1..8 with any direction (8 when none, then gated off)
-  const int j = __builtin_ctz(e8 | (1u << (kDashAllowFrame - 1)));
-  const bool neutral = ((~E >> (j + 1)) & win) != 0;  // some input[i+1 .. i+8] with neither direction
-  const bool isF = (F >> j) & 1, isB = (B >> j) & 1;
-  const bool found = e8 != 0;
-  e.fdash = found & ((r0 & 2) != 0) & ((r1 & 2) == 0) & !isB & isF & neutral;
-  e.bdash = found & ((r0 & 1) != 0) & ((r1 & 1) == 0) & !isF & isB & neutral;
+  const uint32_t j = (uint32_t)__builtin_ctz((E & win) | (1u << (kDashAllowFrame - 1)));
+  const uint32_t neutral = min((~E >> (j + 1)) & win, 1u);  // some input[j+2 .. j+9] with neither direction
+  const uint32_t isF = ((F & win) >> j) & 1u, isB = ((B & win) >> j) & 1u;
+  const uint32_t fd = isF & ~isB & neutral & (r0 >> 1) & ~F;  // forward now, not on input[1]
+  const uint32_t bd = isB & ~isF & neutral & r0 & ~B;         // backward now, not on input[1]
+  e.dash = (fd & 1u) | ((bd & 1u) << 1);
   return e;
 }
 
@@ -352,10 +356,7 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   const bool ended = f.frame >= ai_frame_count(ai);
   const bool inwin = (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai));
   const uint32_t cls = ended ? 2u : (inwin ? 1u : 0u);
-  const uint32_t atk = e.special ? 1u : (e.atk_down ? 2u : 0u);
-  const uint32_t dash = e.fdash ? 1u : (e.bdash ? 2u : 0u);
-  const uint32_t held = (uint32_t)e.back | ((uint32_t)e.fwd << 1);
-  const uint32_t idx = ((uint32_t)f.act << 8) | ((9u * cls + 3u * atk + dash) << 3) | (held << 1) | (uint32_t)f.prox;
+  const uint32_t idx = ((uint32_t)f.act << 8) | ((9u * cls + 3u * e.atk + e.dash) << 3) | (e.held << 1) | (uint32_t)f.prox;
   uint32_t q = sT.req_table[idx];
   uint32_t r0 = ai_rec0(action_info(early ? a0 : 0));
   asm volatile("" : "+v"(q), "+v"(r0));  // both reads in flight together
@@ -367,7 +368,7 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   f.frame = set ? 0 : f.frame;
   f.hits = set ? 0 : f.hits;
   f.rsv = set ? NONE : f.rsv;
-  f.in_back = early ? f.in_back : e.back;  // for proximity guard (F:263)
+  f.in_back = early ? f.in_back : (e.held & 1u) != 0;  // for proximity guard (F:263)
   f.prox = early ? f.prox : false;         // F:285
   *rec = early ? r0 : ((q >> 12) & 255u);
   return set;
