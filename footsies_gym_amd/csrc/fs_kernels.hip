@@ -69,7 +69,7 @@ struct Fighter {
   // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
   // the fighter their world x (y == rect.y since position.y is always 0)
   int rec;        // FrameRec index of (action, frame)
-  uint32_t info;  // FrameRec::info (box counts, hitbox attack bits)
+
   float px, ux0, ux1, hx0, hx1;
   float pw, pymin, pymax;  // pushbox width, yMin, yMax of the record
 };
@@ -407,7 +407,6 @@ __device__ __forceinline__ int frame_record(const Fighter& f) {
 // the fighter's facing (x offsets pre-signed): basePosition.x + dataRect.x * sign.
 template <int FM>
 __device__ __forceinline__ void update_boxes(Fighter& f, const FrameRec& R) {
-  f.info = R.info;
   f.pw = R.push.y;
   f.pymin = R.push.z;
   f.pymax = R.push.w;
@@ -480,8 +479,9 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
 // F:408-420); a proximity box only flags proximity, a real box is a hit and ends
 // the scan.  Branch-free over the 2x2 box pairs: the hit's attack is the first real
 // box that overlaps, and proximity only matters when nothing hit.  The overlaps do
-// not depend on the attacker's hit count, so they are computed once (`BoxHits`) and
-// resolved for a given hit count by `resolve`.
+// not depend on the attacker's hit count, so they are computed once (`BoxHits`); the
+// resolution for every hit count is one entry of kTables.resolve per (attacker record,
+// overlaps), generated offline (tools/gen_tables.py).
 struct HitTest {
   bool hit, prox;
   int atk;
@@ -489,12 +489,11 @@ struct HitTest {
 
 struct BoxHits {
   bool any0, any1;  // hitbox j overlaps some defender hurtbox
-  uint32_t b0, b1;  // hitbox j bits: attack idx 2b | proximity 1b | numberOfHit 2b
 };
 
 template <int FM>
-__device__ __forceinline__ BoxHits box_hits(uint32_t att_info, Box4 h0, Box4 h1, float hx0, float hx1,
-                                            uint32_t def_info, Box4 u0, Box4 u1, float ux0, float ux1) {
+__device__ __forceinline__ BoxHits box_hits(Box4 h0, Box4 h1, float hx0, float hx1, Box4 u0, Box4 u1, float ux0,
+                                            float ux1) {
   // BoxBase.Overlaps (F:17-25) per pair, with each box's xMin / xMax computed once.  Absent
   // boxes (past the record's hurt / hit count) carry an empty y-extent, yMin = +inf and
   // yMax = -inf (tools/gen_tables.py), so their pairs fail the y-test without count checks.
@@ -506,23 +505,9 @@ __device__ __forceinline__ BoxHits box_hits(uint32_t att_info, Box4 h0, Box4 h1,
     return (omax >= smin) & (omin <= smax) & (o.w >= s.z) & (o.z <= s.w);
   };
   BoxHits r;
-  r.b0 = (att_info >> 4) & 31;
-  r.b1 = (att_info >> 9) & 31;
   r.any0 = ov(h0min, h0max, h0, u0min, u0max, u0) | ov(h0min, h0max, h0, u1min, u1max, u1);
   r.any1 = ov(h1min, h1max, h1, u0min, u0max, u0) | ov(h1min, h1max, h1, u1min, u1max, u1);
   return r;
-}
-
-__device__ __forceinline__ HitTest resolve(const BoxHits& r, int att_hits) {
-  const bool any0 = r.any0 & (att_hits < (int)(r.b0 >> 3));  // CanAttackHit
-  const bool any1 = r.any1 & (att_hits < (int)(r.b1 >> 3));
-  const bool p0 = (r.b0 >> 2) & 1, p1 = (r.b1 >> 2) & 1;
-  const bool hit0 = any0 & !p0, hit1 = any1 & !p1;
-  HitTest t;
-  t.hit = hit0 | hit1;
-  t.atk = hit0 ? (int)(r.b0 & 3) : (int)(r.b1 & 3);
-  t.prox = (any0 & p0) | (any1 & p1);
-  return t;
 }
 
 // ---------------------------------------------------------------------------
@@ -859,21 +844,30 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
 // the frame record (one round trip) rather than here.
 template <int FM>
 __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, Box4 my_hurt0, Box4 my_hurt1,
-                                                         Box4 their_hit0, Box4 their_hit1) {
-  const uint32_t o_info = xpair(f.info);
+                                                         Box4 their_hit0, Box4 their_hit1, uint32_t o_rec) {
   // (no wave-level skip: absent hitboxes have empty y-extents and never overlap)
   const int o_hits = xpair(f.hits);
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
-  const BoxHits bh = box_hits<FM>(o_info, their_hit0, their_hit1, o_hx0, o_hx1, f.info, my_hurt0, my_hurt1,
-                                  f.ux0, f.ux1);
+  const BoxHits bh = box_hits<FM>(their_hit0, their_hit1, o_hx0, o_hx1, my_hurt0, my_hurt1, f.ux0, f.ux1);
   // phase A (P1 attacks P2) is resolved on the P2 lane; its outcome crosses to P1, whose lane
   // then resolves phase B (P2 attacks P1) with P2's hit count after phase A
-  const HitTest tA = resolve(bh, o_hits);
+  // the resolution for both phases from one table entry of the attacker's record
+  // (kTables.resolve, tools/gen_tables.py): nibble h = the outcome at attacker hit count h
+  const uint32_t tab = sT.resolve[(o_rec << 2) | ((uint32_t)bh.any0 << 1) | (uint32_t)bh.any1];
+  auto resolve_at = [&](int hits) {
+    const uint32_t nib = tab >> (4 * hits);
+    HitTest t;
+    t.hit = nib & 1u;
+    t.atk = (int)((nib >> 1) & 3u);
+    t.prox = (nib >> 3) & 1u;
+    return t;
+  };
+  const HitTest tA = resolve_at(o_hits);
   // (every exchange is its own statement on both lanes: inside a select the compiler may run
   // the DPP move under a one-lane exec mask, and a disabled source lane reads as 0)
   const uint32_t partner_hitA = xpair((uint32_t)tA.hit);
   const bool hitA = k == 1 ? tA.hit : (partner_hitA & 1u) != 0;
-  const HitTest tB = resolve(bh, hitA ? 0 : o_hits);
+  const HitTest tB = resolve_at(hitA ? 0 : o_hits);
   // each lane is the defender of exactly one phase: one NotifyDamaged per lane.  Order per
   // fighter as in the reference: P1 gets NotifyAttackHit (A) before its NotifyDamaged (B);
   // P2 its NotifyDamaged (A) before NotifyAttackHit (B).
@@ -1072,7 +1066,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   // consumed here, unconditionally, so the reads stay where they were issued (next to the
   // frame record) instead of being sunk into the collision's branch
   asm volatile("" ::"v"(my_hurt0), "v"(my_hurt1), "v"(their_hit0), "v"(their_hit1));
-  hitbox_hurtbox_collision<FM>(L.f, k, my_hurt0, my_hurt1, their_hit0, their_hit1);
+  hitbox_hurtbox_collision<FM>(L.f, k, my_hurt0, my_hurt1, their_hit0, their_hit1, (uint32_t)o_rec);
   // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes
   const uint32_t mine = (uint32_t)L.f.vital | ((uint32_t)L.f.guard << 2) | ((uint32_t)guard_before << 4);
   const uint32_t theirs = xpair(mine);
