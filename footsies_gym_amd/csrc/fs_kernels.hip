@@ -69,7 +69,6 @@ struct Fighter {
   // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
   // the fighter their world x (y == rect.y since position.y is always 0)
   int rec;        // FrameRec index of (action, frame)
-
   float px, ux0, ux1, hx0, hx1;
   float pw, pymin, pymax;  // pushbox width, yMin, yMax of the record
 };
