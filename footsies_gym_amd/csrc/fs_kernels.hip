@@ -593,8 +593,9 @@ __device__ __forceinline__ bool attack_forced(uint32_t b, uint32_t opp) {
   return (((b == 1 ? kAny | kMid : kAny) >> opp) & 1u) != 0;
 }
 
-// The bot as tables (staged into LDS with the frame data): plan inputs as 2-bit codes,
-// one draw descriptor per bucket, plan lengths.
+// The bot as tables (staged into LDS with the frame data), per queue q (0 = attack, 1 =
+// movement): plan inputs as 2-bit codes (movement: Left / Right bits; attack: 1 = Attack
+// pressed), one draw descriptor per distance bucket, plan lengths.
 struct alignas(16) BotDraw {
   uint32_t map;    // nibble r = the plan drawn for r
   uint32_t magic;  // ceil(2^23 / n) (< 2^23): floor(v n^-1) = (v magic) >> 23 for v < 2^20, n < 8
@@ -602,10 +603,9 @@ struct alignas(16) BotDraw {
   uint32_t c16;    // 65536 % n
 };
 struct alignas(16) BotTables {
-  BotDraw move[5], attack[5];
-  uint32_t move_codes[7][8];  // plan p, index i: input bits at 2 (i & 15) of word i >> 4 (rows padded to 32 B)
-  uint8_t move_len[8], attack_len[8], attack_hold[8];
-  uint32_t pad[2];
+  BotDraw draw[2][5];       // [queue][bucket]
+  uint32_t codes[2][8][8];  // [queue][plan][i >> 4]: the input of index i at bits 2 (i & 15)
+  uint8_t len[2][8];        // [queue][plan]
 };
 constexpr BotDraw make_draw(uint32_t n, uint32_t map) {
   return BotDraw{map, (uint32_t)(((1u << 23) + n - 1) / n), n, 65536u % n};
@@ -616,20 +616,22 @@ constexpr BotTables make_bot_tables() {
     uint32_t mm = 0, ma = 0;
     for (uint32_t r = 0; r < move_draw_n(b); r++) mm |= move_draw_plan(b, r) << (4 * r);
     for (uint32_t r = 0; r < attack_draw_n(b); r++) ma |= attack_draw_plan(b, r) << (4 * r);
-    t.move[b] = make_draw(move_draw_n(b), mm);
-    t.attack[b] = make_draw(attack_draw_n(b), ma);
+    t.draw[1][b] = make_draw(move_draw_n(b), mm);
+    t.draw[0][b] = make_draw(attack_draw_n(b), ma);
   }
   for (uint32_t p = 0; p < 7; p++) {
-    t.move_len[p] = (uint8_t)move_plan_len(p);
-    for (uint32_t i = 0; i < move_plan_len(p); i++) t.move_codes[p][i >> 4] |= move_plan_input(p, i) << (2 * (i & 15));
+    t.len[1][p] = (uint8_t)move_plan_len(p);
+    for (uint32_t i = 0; i < move_plan_len(p); i++) t.codes[1][p][i >> 4] |= move_plan_input(p, i) << (2 * (i & 15));
   }
-  for (uint32_t p = 0; p < 5; p++) {
-    t.attack_len[p] = (uint8_t)attack_plan_len(p);
-    t.attack_hold[p] = (uint8_t)attack_plan_hold(p);
+  for (uint32_t p = 0; p < 5; p++) {  // Attack held for the first frames; AP_TWO_HIT presses again at index 4
+    t.len[0][p] = (uint8_t)attack_plan_len(p);
+    for (uint32_t i = 0; i < attack_plan_len(p); i++)
+      t.codes[0][p][i >> 4] |= (uint32_t)((i < attack_plan_hold(p)) | ((p == AP_TWO_HIT) & (i == 4))) << (2 * (i & 15));
   }
   return t;
 }
-static_assert(move_plan_len(MP_FAR1) <= 6 * 16, "move plans fit six code words");
+static_assert(move_plan_len(MP_FAR1) <= 8 * 16 && attack_plan_len(AP_DELAY_SPECIAL) <= 8 * 16,
+              "plans fit eight code words");
 __constant__ const BotTables kBot = make_bot_tables();
 __shared__ BotTables sBot;
 
@@ -675,10 +677,14 @@ __device__ __forceinline__ uint32_t draw_mod(uint32_t x, const BotDraw& d) {
 // getNextAIInput (AI:41-66) for the P2 bot.  The ascending copy loop of
 // UpdateFightState (AI:358-361) leaves fightStates[5] == the *previous* call's
 // state, so the bot keeps one FightState: (distance, opponent action).
+// The two lanes of an arena share the bot: each runs one of its two input queues (the P1 lane
+// the attack queue, the P2 lane the movement queue) and both keep replicas of the RNG and of
+// the previous FightState, so one pass of the same instructions serves both queues.
 struct Bot {
-  uint4 rng;
-  uint32_t mplan, midx, aplan, aidx, prev_opp;  // plans stored + 1 (0 = queue empty)
-  float prev_dist;
+  uint4 rng;               // replica on both lanes
+  uint32_t plan, idx;      // this lane's queue: plan stored + 1 (0 = empty), index into it
+  uint32_t prev_opp;       // replica
+  float prev_dist;         // replica
 };
 
 // Mathf.Abs(fighter2.x - fighter1.x) (AI:370-373)
@@ -687,21 +693,24 @@ __device__ __forceinline__ float bot_distance(float x1, float x2) {
   return fabsf(fsub<FM>(x2, x1));
 }
 
-// Branch-free: both queues' next inputs from the code tables, both possible draws computed
-// (movement first, then attack -- the order the C# calls Random.Range) and the RNG state
-// advanced by the number actually taken.
-__device__ __forceinline__ uint32_t bot_next_input(Bot& b, float dist, uint32_t opp_act) {
+// Branch-free over the pair: this lane's queue input from the code tables, both queues' busy
+// flags (one exchange), both possible draws for the RNG (movement first, then attack -- the order
+// the C# calls Random.Range), this queue's draw, and the RNG advanced by the number taken.
+// q = this lane's queue (0 = attack on the P1 lane, 1 = movement on the P2 lane).  Both lanes of
+// the pair must call it (it exchanges with the partner); it returns the bot's input on both.
+__device__ __forceinline__ uint32_t xpair(uint32_t v);
+__device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dist, uint32_t opp_act) {
   const float d = b.prev_dist;
   const uint32_t opp = b.prev_opp;
   b.prev_dist = dist;
   b.prev_opp = opp_act;
   const uint32_t bucket = d > 4.0f ? 0u : d > 3.0f ? 1u : d > 2.5f ? 2u : d > 2.0f ? 3u : 4u;
-  const bool mbusy = b.mplan != 0, abusy = b.aplan != 0;
-  const uint32_t mp = mbusy ? b.mplan - 1 : 0u, ap = abusy ? b.aplan - 1 : 0u;
-  const uint32_t mi = b.midx, ai = b.aidx;
-  const uint32_t in_m = (sBot.move_codes[mp][mi >> 4] >> (2 * (mi & 15))) & 3u;  // 32-B rows: a shift, not a multiply
-  const bool press = (ai < sBot.attack_hold[ap]) | ((ap == AP_TWO_HIT) & (ai == 4));
-  const uint32_t input = (mbusy ? in_m : 0u) | ((abusy & press) ? IN_ATTACK : 0u);
+  const bool busy = b.plan != 0;
+  const uint32_t p = busy ? b.plan - 1 : 0u, i = b.idx;
+  const uint32_t code = (sBot.codes[q][p][i >> 4] >> (2 * (i & 15))) & 3u;
+  const uint32_t mine = busy ? (q ? code : code << 2) : 0u;  // Left / Right bits, or IN_ATTACK
+  const bool o_busy = xpair((uint32_t)busy) != 0;
+  const bool mbusy = q ? busy : o_busy, abusy = q ? o_busy : busy;
   const bool forced = attack_forced(bucket, opp);
   const bool dm = !mbusy, da = !abusy & !forced;
   uint4 s1 = b.rng;
@@ -710,15 +719,13 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, float dist, uint32_t 
   const uint32_t x2 = rng_next(s2);
   const uint4 s0 = b.rng;
   b.rng = (dm & da) ? s2 : (dm | da) ? s1 : s0;
-  const BotDraw wm = sBot.move[bucket], wa = sBot.attack[bucket];
-  const uint32_t new_m = (wm.map >> (4 * draw_mod(x1, wm))) & 15u;
-  const uint32_t new_a = forced ? (uint32_t)AP_TWO_HIT : (wa.map >> (4 * draw_mod(dm ? x2 : x1, wa))) & 15u;
-  const uint32_t mi1 = mi + 1, ai1 = ai + 1;
-  b.mplan = mbusy ? (mi1 == sBot.move_len[mp] ? 0u : b.mplan) : new_m + 1;
-  b.midx = mbusy ? mi1 : 0u;
-  b.aplan = abusy ? (ai1 == sBot.attack_len[ap] ? 0u : b.aplan) : new_a + 1;
-  b.aidx = abusy ? ai1 : 0u;
-  return input;
+  const BotDraw w = sBot.draw[q][bucket];
+  const uint32_t drawn = (w.map >> (4 * draw_mod((!q & dm) ? x2 : x1, w))) & 15u;
+  const uint32_t newp = (!q & forced) ? (uint32_t)AP_TWO_HIT : drawn;
+  const uint32_t i1 = i + 1;
+  b.plan = busy ? (i1 == sBot.len[q][p] ? 0u : b.plan) : newp + 1;
+  b.idx = busy ? i1 : 0u;
+  return mine | xpair(mine);
 }
 
 // ---------------------------------------------------------------------------
@@ -770,10 +777,8 @@ __device__ __forceinline__ void load_lane(Lane& L, const DevState& s, int a, uin
   if constexpr (BOT) {  // both lanes read the same 24 B (one cache line); P2 uses it
     L.bot.rng = s.rng[a];
     const uint2 b = s.bot[a];
-    L.bot.mplan = b.x & 7;
-    L.bot.midx = (b.x >> 3) & 127;
-    L.bot.aplan = (b.x >> 10) & 7;
-    L.bot.aidx = (b.x >> 13) & 127;
+    L.bot.plan = k ? (b.x & 7) : ((b.x >> 10) & 7);  // P2 lane: movement queue, P1 lane: attack queue
+    L.bot.idx = k ? ((b.x >> 3) & 127) : ((b.x >> 13) & 127);
     L.bot.prev_opp = (b.x >> 20) & 31;
     L.bot.prev_dist = __uint_as_float(b.y);
   }
@@ -794,11 +799,11 @@ __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int
     s.cum[a] = L.cum;
   }
   if constexpr (BOT) {
+    const Bot& b = L.bot;
+    const uint32_t mine = b.plan | (b.idx << 3), other = xpair(mine);  // the partner's queue
     if (L.k == 1) {
-      const Bot& b = L.bot;
       s.rng[a] = b.rng;
-      s.bot[a] = make_uint2(b.mplan | (b.midx << 3) | (b.aplan << 10) | (b.aidx << 13) | (b.prev_opp << 20),
-                            __float_as_uint(b.prev_dist));
+      s.bot[a] = make_uint2(mine | (other << 10) | (b.prev_opp << 20), __float_as_uint(b.prev_dist));
     }
   }
 }
@@ -936,7 +941,7 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
   const float x1 = L.k == 0 ? L.f.x : o_x, x2 = L.k == 0 ? o_x : L.f.x;
   const uint32_t p1_act = L.k == 0 ? (uint32_t)L.f.act : o_act;
   if constexpr (BOT) {  // BattleAI.Reset (AI:393-403)
-    L.bot.mplan = L.bot.midx = L.bot.aplan = L.bot.aidx = 0;
+    L.bot.plan = L.bot.idx = 0;
     L.bot.prev_dist = bot_distance<FM>(x1, x2);
     L.bot.prev_opp = p1_act;
   }
@@ -953,7 +958,8 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
   L.frame_count = -1;
   L.rec_count = 0;
   if constexpr (BOT) {
-    if (L.k == 1) L.act = bot_next_input(L.bot, bot_distance<FM>(x1, x2), p1_act);
+    const uint32_t in = bot_next_input(L.bot, L.k, bot_distance<FM>(x1, x2), p1_act);
+    L.act = L.k == 1 ? in : L.act;
   }
 }
 
@@ -1103,7 +1109,10 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     if constexpr (BOT) {  // TrainingManager.Step -> RequestNextInput -> getNextAIInput
       const float o_x = xpair(L.f.x);
       const uint32_t o_act = xpair((uint32_t)L.f.act);
-      if (k == 1) L.act = bot_next_input(L.bot, bot_distance<FM>(o_x, L.f.x), o_act);
+      const float x1 = k == 0 ? L.f.x : o_x, x2 = k == 0 ? o_x : L.f.x;
+      const uint32_t p1_act = k == 0 ? (uint32_t)L.f.act : o_act;
+      const uint32_t in = bot_next_input(L.bot, k, bot_distance<FM>(x1, x2), p1_act);
+      L.act = k == 1 ? in : L.act;
     }
     L.has_term = false;
   }
@@ -1241,7 +1250,7 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
     L.has_term = true;
     L.cum = 0.0;
     L.bot.rng = rng_init((int32_t)(uint32_t)(p.base_seed + (uint64_t)a));
-    L.bot.mplan = L.bot.midx = L.bot.aplan = L.bot.aidx = L.bot.prev_opp = 0;
+    L.bot.plan = L.bot.idx = L.bot.prev_opp = 0;
     L.bot.prev_dist = 0.0f;
   } else {
     load_lane<BOT>(L, p.st, a, k);
