@@ -735,7 +735,7 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dis
 // reward) exchange the partner's values with one DPP quad_perm [1,0,3,2] move
 // per 32-bit value.  Arena-level fields (frameCount, recording count, reward
 // accumulator, reset flags) are kept as identical replicas on both lanes and
-// stored by lane k = 0; the bot lives on the P2 lane.  Every exchange sits in
+// stored by lane k = 0; the bot's two queues are split over the pair.  Every exchange sits in
 // control flow that is uniform across a pair, so the partner lane is active.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t xpair(uint32_t v) {
@@ -754,7 +754,7 @@ struct Lane {
   uint32_t rec;       // this player's recordingPnInput[index - 1]
   uint32_t act;       // this player's TrainingActor.GetInput()
   AInfo ai;           // ActionInfo of f.act (reloaded at the end of every tick)
-  Bot bot;            // P2 lane, FS_P2_BOT only
+  Bot bot;            // FS_P2_BOT only: this lane's queue + replicas (see Bot)
 };
 
 template <bool BOT>
