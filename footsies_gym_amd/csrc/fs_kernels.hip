@@ -373,15 +373,13 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   return set;
 }
 
-// UpdateMovement (F:291-319).  FORWARD / BACKWARD walk at the fighter speeds; any
-// other action takes the first movement window's velocity (0 = none).  BACKWARD's
-// `pos -= s*sign*dt` is `pos + (-s)*sign*dt` bit for bit (negation is exact and
-// round-to-nearest is symmetric), so one expression covers all three; `v*sign` is exact
-// too, so the velocities arrive pre-signed (walk speeds per lane, the facing-left frame
-// records negated) and the step is pos + v*dt.
+// UpdateMovement (F:291-319).  FORWARD / BACKWARD walk at the fighter speeds, any other action
+// takes the first movement window's velocity (0 = none).  BACKWARD's `pos -= s*sign*dt` is
+// `pos + (-s)*sign*dt` bit for bit (negation is exact and round-to-nearest is symmetric), and
+// `v*sign` is exact too, so every case is pos + v*dt with v pre-signed in the frame record:
+// tools/gen_tables.py stores the walk speeds in the FORWARD / BACKWARD records.
 template <int FM>
-__device__ __forceinline__ void update_movement(Fighter& f, float walk_fwd, float walk_back, float rec_vel) {
-  const float v = f.act == A_FORWARD ? walk_fwd : f.act == A_BACKWARD ? walk_back : rec_vel;
+__device__ __forceinline__ void update_movement(Fighter& f, float v) {
   float nx;
   if constexpr (FM == FS_FLOAT_DOUBLE) nx = (float)__dadd_rn((double)f.x, __dmul_rn((double)v, (double)kDt));
   else nx = __fadd_rn(f.x, __fmul_rn(v, kDt));
@@ -1047,8 +1045,6 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.rec = L.act;
     L.rec_count++;
   }
-  const float walk_fwd = k == 0 ? kForwardSpeed : -kForwardSpeed;    // speed * sign
-  const float walk_back = k == 0 ? -kBackwardSpeed : kBackwardSpeed;  // -speed * sign
   const InputEval e = update_input(L.f, L.act, (int)k);
   const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
   increment_action_frame(L.f, ai);
@@ -1064,7 +1060,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   const Box4 my_hurt0 = box4(R.hurt[0]), my_hurt1 = box4(R.hurt[1]);
   const FrameRec& O = frame_rec(0, (uint32_t)o_rec);
   const Box4 their_hit0 = box4(O.hit[0]), their_hit1 = box4(O.hit[1]);
-  update_movement<FM>(L.f, walk_fwd, walk_back, R.vel);
+  update_movement<FM>(L.f, R.vel);
   update_boxes<FM>(L.f, R);
   push_character_vs_character<FM>(L.f, k);
   push_character_vs_background<FM>(L.f);
