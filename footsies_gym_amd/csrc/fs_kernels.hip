@@ -9,7 +9,7 @@
 //
 // Frame data is one ~21 KB image staged into LDS per block: per action a 16-B
 // ActionInfo (frame count, loop, cancel window), per (action, frame) an index into
-// 51 de-duplicated 96-B frame records holding every box's geometry, the velocity and
+// 53 de-duplicated 96-B frame records holding every box's geometry, the velocity and
 // the hitbox attack bits -- the window scans of ActionData.cs:87-168 resolved offline
 // (tools/gen_tables.py) -- and the request chain's outcome per (action, window state,
 // inputs).  A tick's dependent LDS round trips: action info, then the record index and
