@@ -7,7 +7,7 @@
 //
 //   load (coalesced 4/8/16-B per lane) -> n ticks in registers -> store
 //
-// Frame data is one ~21 KB image staged into LDS per block: per action a 16-B
+// Frame data is one ~30 KB image staged into LDS per block: per action a 16-B
 // ActionInfo (frame count, loop, cancel window), per (action, frame) an index into
 // 53 de-duplicated 96-B frame records holding every box's geometry, the velocity and
 // the hitbox attack bits -- the window scans of ActionData.cs:87-168 resolved offline
