@@ -1317,11 +1317,42 @@ OR_EXPORT int or_get_state(or_handle C, fs_arena_state* out) {
    from what fs_arena_state carries -- directions of input[0..15], Attack over the held run
    input[0..hold-1] -- with zeros beyond; inputDown / inputUp follow from input (F:182-184).
    Boxes and velocity_x are left for the next UpdateBoxes / UpdateMovement to set.  A
-   pending terminal arena resumes in KO with its timer at 0 (BC:303-306).  The scripted
-   bot's queues and FightState ring are not rebuilt here: FS_E_UNSUPPORTED for FS_P2_BOT. */
+   pending terminal arena resumes in KO with its timer at 0 (BC:303-306).  With the scripted
+   bot, its queues are rebuilt by enqueueing each plan (set_move_plan / set_attack_plan) and
+   popping the inputs already consumed, and every FightState slot holds the previous call's
+   state: getNextAIInput's ascending copy loop overwrites slots 1..9 with slot 0 before it
+   reads slot 5 (AI:358-361), so slot 0 is all a later call can observe. */
+static void bot_set_state(arena_t* A, const fs_arena_state* s) {
+  bot_t* b = &A->bot;
+  memcpy(A->rng, s->rng, sizeof A->rng);
+  q_clear(&b->move_q);
+  q_clear(&b->attack_q);
+  b->move_plan = b->attack_plan = -1;
+  b->move_len = b->attack_len = 0;
+  if (s->move_plan >= 0) {
+    set_move_plan(b, s->move_plan);
+    for (int i = 0; i < s->move_index && b->move_q.count > 0; i++) q_pop(&b->move_q);
+  }
+  if (s->attack_plan >= 0) {
+    set_attack_plan(b, s->attack_plan);
+    for (int i = 0; i < s->attack_index && b->attack_q.count > 0; i++) q_pop(&b->attack_q);
+  }
+  fight_state_t prev;
+  memset(&prev, 0, sizeof prev);
+  const int opp = s->prev_opponent_action;
+  prev.valid = 1;
+  prev.distance_x = s->prev_distance;
+  prev.opp_damage = opp == DAMAGE;
+  prev.opp_guard_break = opp == GUARD_BREAK;
+  prev.opp_blocking = opp == GUARD_CROUCH || opp == GUARD_STAND || opp == GUARD_M;
+  prev.opp_normal_attack = opp == N_ATTACK || opp == B_ATTACK;
+  prev.opp_special_attack = opp == N_SPECIAL || opp == B_SPECIAL;
+  prev.opp_action = opp;
+  for (int i = 0; i < 10; i++) b->fs[i] = prev;
+}
+
 OR_EXPORT int or_set_state(or_handle C, const fs_arena_state* in) {
   if (!C || !in) return FS_E_INVALID;
-  if (C->cfg.p2_mode == FS_P2_BOT) return FS_E_UNSUPPORTED;
   for (int i = 0; i < C->n; i++) {
     arena_t* A = &C->a[i];
     const fs_arena_state* s = &in[i];
@@ -1365,6 +1396,7 @@ OR_EXPORT int or_set_state(or_handle C, const fs_arena_state* in) {
     A->cum_reward = s->cumulative_reward;
     A->round_state = s->reset_pending ? RS_KO : RS_FIGHT;
     A->timer = 0.0f;
+    if (C->cfg.p2_mode == FS_P2_BOT) bot_set_state(A, s);
     A->cur_state = get_environment_state(A);
   }
   return FS_OK;

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from footsies_gym_amd import _abi
-from tests.parity_utils import compare_outputs, compare_states
+from tests.parity_utils import compare_outputs, compare_states, random_states
 
 pytestmark = pytest.mark.gpu
 
@@ -86,58 +86,11 @@ def test_lockstep_4096_bot_long(oracle_lib):
     run_lockstep(sim, ora, 10000, np.random.default_rng(123), state_every=500, sticky=0.5)
 
 
-ACTION_FRAMES = {0: 24, 1: 24, 2: 24, 10: 16, 11: 22, 100: 22, 105: 21, 110: 44, 115: 55, 200: 17, 301: 23,
-                 305: 15, 306: 15, 310: 36, 350: 1, 500: 500, 510: 33}  # frameCount per actionID (data/f00.json)
-LOOPING = {0, 1, 2, 350, 510}
-MOVE_PLAN_LEN, ATTACK_PLAN_LEN = [30, 90, 56, 70, 33, 60, 63], [30, 19, 23, 61, 121]
-
-
-def random_states(n, rng):
-    """Arbitrary loadable arena states (fs_arena_state), not only ones reachable from a reset:
-    any action at any frame up to its frameCount, buffered / reserved actions, hitstun, latches,
-    hasWon, saturated recordings, random histories and bot queues -- the paths a played match
-    reaches rarely (the hasWon request, reserve / buffer takes, DEAD past frame 63)."""
-    st = np.zeros(n, dtype=np.ctypeslib.as_array((_abi.fs_arena_state * 1)()).dtype)
-    ids = np.array(sorted(ACTION_FRAMES), dtype=np.int32)
-    for k in range(2):
-        f = st["f"][:, k]
-        f["position_x"] = rng.uniform(-4.5, 4.5, n).astype(np.float32)
-        f["action_id"] = rng.choice(ids, n)
-        top = np.array([ACTION_FRAMES[a] - (1 if a in LOOPING else 0) for a in f["action_id"]])
-        f["action_frame"] = (rng.random(n) * (top + 1)).astype(np.int32)
-        f["hit_count"] = rng.integers(0, 3, n)
-        f["hitstun"] = np.where(rng.random(n) < 0.5, 0, rng.integers(0, 31, n))
-        f["vital"] = (rng.random(n) < 0.95).astype(np.int32)
-        f["guard"] = rng.integers(0, 4, n)
-        f["buffer_action_id"] = np.where(rng.random(n) < 0.6, -1, rng.choice(ids, n))
-        f["reserve_action_id"] = np.where(rng.random(n) < 0.7, -1, rng.choice(ids, n))
-        f["input_dir_history"] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
-        f["attack_hold"] = rng.integers(0, 64, n)
-        f["is_input_backward"] = rng.integers(0, 2, n)
-        f["is_reserve_proximity_guard"] = rng.integers(0, 2, n)
-        f["has_won"] = (rng.random(n) < 0.1).astype(np.uint8)
-    st["frame_count"] = rng.integers(0, 5000, n)
-    st["recording_count"] = np.where(rng.random(n) < 0.2, 18000, rng.integers(0, 18000, n))
-    st["recording_last"] = rng.integers(0, 8, (n, 2))
-    st["actor_input"] = rng.integers(0, 8, (n, 2))
-    st["cumulative_reward"] = rng.integers(-3, 4, n) * 0.3
-    st["rng"] = rng.integers(1, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
-    mp = rng.integers(-1, 7, n)
-    ap = rng.integers(-1, 5, n)
-    st["move_plan"], st["attack_plan"] = mp, ap
-    st["move_index"] = np.where(mp < 0, 0, (rng.random(n) * np.take(MOVE_PLAN_LEN, np.maximum(mp, 0))).astype(int))
-    st["attack_index"] = np.where(ap < 0, 0,
-                                  (rng.random(n) * np.take(ATTACK_PLAN_LEN, np.maximum(ap, 0))).astype(int))
-    st["prev_distance"] = rng.uniform(0.0, 9.0, n).astype(np.float32)
-    st["prev_opponent_action"] = rng.choice(ids, n)
-    return st
-
-
-@pytest.mark.parametrize("p2", ["external", "noop"])
+@pytest.mark.parametrize("p2", ["external", "bot", "noop"])
 def test_lockstep_from_random_loaded_states(oracle_lib, p2):
-    """STATE_LOAD of arbitrary states into both, then lockstep: the table-driven request chain
-    and hit resolution agree with the oracle's restatement on the rare paths too.  (The oracle
-    does not rebuild the scripted bot's queues from a loaded state, so P2 is external / noop.)"""
+    """STATE_LOAD of arbitrary states into both, then lockstep: the table-driven request chain,
+    hit resolution and the bot's split queues agree with the oracle's restatement on the rare
+    paths too (the oracle rebuilds the bot's real queues and FightState ring from the state)."""
     n = 4096
     sim, ora = make_pair(oracle_lib, n, p2, seed=21)
     st = random_states(n, np.random.default_rng(77))
