@@ -7,7 +7,7 @@
 //
 //   load (coalesced 4/8/16-B per lane) -> n ticks in registers -> store
 //
-// Frame data is one ~30 KB image staged into LDS per block: per action a 16-B
+// Frame data is one 36 KB image staged into LDS per block: per action a 16-B
 // ActionInfo (frame count, loop, cancel window), per (action, frame) an index into
 // 53 de-duplicated 96-B frame records holding every box's geometry, the velocity and
 // the hitbox attack bits -- the window scans of ActionData.cs:87-168 resolved offline
@@ -476,35 +476,31 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
 // F:408-420); a proximity box only flags proximity, a real box is a hit and ends
 // the scan.  Branch-free over the 2x2 box pairs: the hit's attack is the first real
 // box that overlaps, and proximity only matters when nothing hit.  The overlaps do
-// not depend on the attacker's hit count, so they are computed once (`BoxHits`); the
-// resolution for every hit count is one entry of kTables.resolve per (attacker record,
-// overlaps), generated offline (tools/gen_tables.py).
+// not depend on the attacker's hit count, so they are computed once, as a 4-bit mask
+// (bit 2j+i: attacker hitbox j overlaps defender hurtbox i); the resolution for every
+// hit count is one entry of kTables.resolve per (attacker record, mask), generated
+// offline (tools/gen_tables.py).
 struct HitTest {
   bool hit, prox;
   int atk;
 };
 
-struct BoxHits {
-  bool any0, any1;  // hitbox j overlaps some defender hurtbox
-};
-
+// The x half of BoxBase.Overlaps (F:17-25) per box pair, with each box's xMin / xMax computed
+// once, as mask bits 2j+i.  The y half depends on the two frame records alone (boxes move in x
+// only) and comes from kTables.ybits, which is also 0 for absent boxes (past a record's box
+// count), so no count checks are needed here.
 template <int FM>
-__device__ __forceinline__ BoxHits box_hits(Box4 h0, Box4 h1, float hx0, float hx1, Box4 u0, Box4 u1, float ux0,
-                                            float ux1) {
-  // BoxBase.Overlaps (F:17-25) per pair, with each box's xMin / xMax computed once.  Absent
-  // boxes (past the record's hurt / hit count) carry an empty y-extent, yMin = +inf and
-  // yMax = -inf (tools/gen_tables.py), so their pairs fail the y-test without count checks.
+__device__ __forceinline__ uint32_t box_x_overlaps(Box4 h0, Box4 h1, float hx0, float hx1, Box4 u0, Box4 u1,
+                                                   float ux0, float ux1) {
   const float h0min = fsub<FM>(hx0, h0.y), h0max = fadd<FM>(hx0, h0.y);
   const float h1min = fsub<FM>(hx1, h1.y), h1max = fadd<FM>(hx1, h1.y);
   const float u0min = fsub<FM>(ux0, u0.y), u0max = fadd<FM>(ux0, u0.y);
   const float u1min = fsub<FM>(ux1, u1.y), u1max = fadd<FM>(ux1, u1.y);
-  auto ov = [](float smin, float smax, Box4 s, float omin, float omax, Box4 o) {
-    return (omax >= smin) & (omin <= smax) & (o.w >= s.z) & (o.z <= s.w);
+  auto ov = [](float smin, float smax, float omin, float omax) {
+    return (uint32_t)((omax >= smin) & (omin <= smax));
   };
-  BoxHits r;
-  r.any0 = ov(h0min, h0max, h0, u0min, u0max, u0) | ov(h0min, h0max, h0, u1min, u1max, u1);
-  r.any1 = ov(h1min, h1max, h1, u0min, u0max, u0) | ov(h1min, h1max, h1, u1min, u1max, u1);
-  return r;
+  return ov(h0min, h0max, u0min, u0max) | (ov(h0min, h0max, u1min, u1max) << 1) |
+         (ov(h1min, h1max, u0min, u0max) << 2) | (ov(h1min, h1max, u1min, u1max) << 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -846,16 +842,17 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
 // the frame record (one round trip) rather than here.
 template <int FM>
 __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, Box4 my_hurt0, Box4 my_hurt1,
-                                                         Box4 their_hit0, Box4 their_hit1, uint32_t o_rec) {
+                                                         Box4 their_hit0, Box4 their_hit1, uint32_t o_rec,
+                                                         uint32_t ym) {
   // (no wave-level skip: absent hitboxes have empty y-extents and never overlap)
   const int o_hits = xpair(f.hits);
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
-  const BoxHits bh = box_hits<FM>(their_hit0, their_hit1, o_hx0, o_hx1, my_hurt0, my_hurt1, f.ux0, f.ux1);
+  const uint32_t xm = box_x_overlaps<FM>(their_hit0, their_hit1, o_hx0, o_hx1, my_hurt0, my_hurt1, f.ux0, f.ux1);
   // phase A (P1 attacks P2) is resolved on the P2 lane; its outcome crosses to P1, whose lane
   // then resolves phase B (P2 attacks P1) with P2's hit count after phase A
   // the resolution for both phases from one table entry of the attacker's record
   // (kTables.resolve, tools/gen_tables.py): nibble h = the outcome at attacker hit count h
-  const uint32_t tab = sT.resolve[(o_rec << 2) | ((uint32_t)bh.any0 << 1) | (uint32_t)bh.any1];
+  const uint32_t tab = sT.resolve[(o_rec << 4) | (xm & ym)];
   auto resolve_at = [&](int hits) {
     const uint32_t nib = tab >> (4 * hits);
     HitTest t;
@@ -1060,14 +1057,17 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   const Box4 my_hurt0 = box4(R.hurt[0]), my_hurt1 = box4(R.hurt[1]);
   const FrameRec& O = frame_rec(0, (uint32_t)o_rec);
   const Box4 their_hit0 = box4(O.hit[0]), their_hit1 = box4(O.hit[1]);
+  // the y half of the box-pair overlaps (records only, kTables.ybits)
+  static_assert(kNumFrameRecs <= 64, "ybits rows are 64 records wide");
+  const uint32_t ym = sT.ybits[((uint32_t)o_rec << 6) | (uint32_t)L.f.rec];
   update_movement<FM>(L.f, R.vel);
   update_boxes<FM>(L.f, R);
   push_character_vs_character<FM>(L.f, k);
   push_character_vs_background<FM>(L.f);
   // consumed here, unconditionally, so the reads stay where they were issued (next to the
   // frame record) instead of being sunk into the collision's branch
-  asm volatile("" ::"v"(my_hurt0), "v"(my_hurt1), "v"(their_hit0), "v"(their_hit1));
-  hitbox_hurtbox_collision<FM>(L.f, k, my_hurt0, my_hurt1, their_hit0, their_hit1, (uint32_t)o_rec);
+  asm volatile("" ::"v"(my_hurt0), "v"(my_hurt1), "v"(their_hit0), "v"(their_hit1), "v"(ym));
+  hitbox_hurtbox_collision<FM>(L.f, k, my_hurt0, my_hurt1, their_hit0, their_hit1, (uint32_t)o_rec, ym);
   // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes
   const uint32_t mine = (uint32_t)L.f.vital | ((uint32_t)L.f.guard << 2) | ((uint32_t)guard_before << 4);
   const uint32_t theirs = xpair(mine);
