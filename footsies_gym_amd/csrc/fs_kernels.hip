@@ -351,25 +351,23 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   // The request chain (special / attack F:234-254, dash F:256-259, movement F:265-283, each
   // through RequestAction F:472-510) as one read of kTables.req_table: its outcome depends only
   // on the action, whether it has ended or sits in its cancel window, the attack / dash / held
-  // direction inputs and the proximity latch (tools/gen_tables.py runs the chain for each).
+  // direction inputs and the proximity latch (tools/gen_tables.py runs the chain for each).  An
+  // early return reads the entry "SetCurrentAction(a0)" instead, so both paths merge alike.
   const bool ended = f.frame >= ai_frame_count(ai);
   const bool inwin = (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai));
   const uint32_t cls = ended ? 2u : (inwin ? 1u : 0u);
   const uint32_t idx = ((uint32_t)f.act << 8) | ((9u * cls + 3u * e.atk + e.dash) << 3) | (e.held << 1) | (uint32_t)f.prox;
-  uint32_t q = sT.req_table[idx];
-  uint32_t r0 = ai_rec0(action_info(early ? a0 : 0));
-  asm volatile("" : "+v"(q), "+v"(r0));  // both reads in flight together
-  took = !early & (((q >> 11) & 1u) != 0);
-  const bool bset = !early & (((q >> 10) & 1u) != 0);
-  const bool set = took | early;  // SetCurrentAction ran (F:546-563)
-  f.act = early ? a0 : (took ? (int)(q & 31u) : f.act);
+  const uint32_t q = sT.req_table[early ? (uint32_t)(kReqEarly + a0) : idx];
+  const bool set = ((q >> 11) & 1u) != 0;  // SetCurrentAction ran (F:546-563)
+  const bool bset = ((q >> 10) & 1u) != 0;
+  f.act = set ? (int)(q & 31u) : f.act;
   f.buf = set ? NONE : (bset ? (int)((q >> 5) & 31u) : f.buf);
   f.frame = set ? 0 : f.frame;
   f.hits = set ? 0 : f.hits;
   f.rsv = set ? NONE : f.rsv;
   f.in_back = early ? f.in_back : (e.held & 1u) != 0;  // for proximity guard (F:263)
   f.prox = early ? f.prox : false;         // F:285
-  *rec = early ? r0 : ((q >> 12) & 255u);
+  *rec = (q >> 12) & 255u;
   return set;
 }
 
@@ -480,11 +478,6 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
 // (bit 2j+i: attacker hitbox j overlaps defender hurtbox i); the resolution for every
 // hit count is one entry of kTables.resolve per (attacker record, mask), generated
 // offline (tools/gen_tables.py).
-struct HitTest {
-  bool hit, prox;
-  int atk;
-};
-
 // The x half of BoxBase.Overlaps (F:17-25) per box pair, with each box's xMin / xMax computed
 // once, as mask bits 2j+i.  The y half depends on the two frame records alone (boxes move in x
 // only) and comes from kTables.ybits, which is also 0 for absent boxes (past a record's box
@@ -840,6 +833,8 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
 // P1 (to pick B's variant), B's result to P2, and each defender's stun to the other.
 // The record boxes (my hurtboxes, the partner's hitboxes) are read from LDS together with
 // the frame record (one round trip) rather than here.
+__device__ __forceinline__ uint32_t bit0_mask(uint32_t v) { return (uint32_t)((int32_t)(v << 31) >> 31); }  // 0 / ~0
+
 template <int FM>
 __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, Box4 my_hurt0, Box4 my_hurt1,
                                                          Box4 their_hit0, Box4 their_hit1, uint32_t o_rec,
@@ -853,27 +848,22 @@ __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k,
   // the resolution for both phases from one table entry of the attacker's record
   // (kTables.resolve, tools/gen_tables.py): nibble h = the outcome at attacker hit count h
   const uint32_t tab = sT.resolve[(o_rec << 4) | (xm & ym)];
-  auto resolve_at = [&](int hits) {
-    const uint32_t nib = tab >> (4 * hits);
-    HitTest t;
-    t.hit = nib & 1u;
-    t.atk = (int)((nib >> 1) & 3u);
-    t.prox = (nib >> 3) & 1u;
-    return t;
-  };
-  const HitTest tA = resolve_at(o_hits);
+  // The entry shifted by the partner's hit count: on the P2 lane phase A's outcome (P1's hit
+  // count); on the P1 lane phase B's, unless phase A hit P2 -- which resets P2's hit count to 0
+  // first (SetCurrentAction), so P1 then reads nibble 0.
   // (every exchange is its own statement on both lanes: inside a select the compiler may run
   // the DPP move under a one-lane exec mask, and a disabled source lane reads as 0)
-  const uint32_t partner_hitA = xpair((uint32_t)tA.hit);
-  const bool hitA = k == 1 ? tA.hit : (partner_hitA & 1u) != 0;
-  const HitTest tB = resolve_at(hitA ? 0 : o_hits);
+  const uint32_t t1 = tab >> (4u * (uint32_t)o_hits);
+  const uint32_t x1 = xpair(t1);
+  const uint32_t hitA = (k == 1 ? t1 : x1) & 1u;
+  const uint32_t t = (k == 0 && hitA) ? tab : t1;  // this lane's phase as the defender
+  const bool my_hit = (t & 1u) != 0;
+  const int my_atk = (int)((t >> 1) & 3u);
+  const bool my_prox = ((t >> 3) & 1u) != 0;
   // each lane is the defender of exactly one phase: one NotifyDamaged per lane.  Order per
   // fighter as in the reference: P1 gets NotifyAttackHit (A) before its NotifyDamaged (B);
   // P2 its NotifyDamaged (A) before NotifyAttackHit (B).
-  const bool my_hit = k == 1 ? tA.hit : tB.hit;
-  const int my_atk = k == 1 ? tA.atk : tB.atk;
-  const bool my_prox = k == 1 ? tA.prox : tB.prox;
-  if (k == 0 && hitA) f.hits++;  // NotifyAttackHit for P1 (F:352-355)
+  f.hits += k == 0 ? (int)hitA : 0;  // NotifyAttackHit for P1 (F:352-355)
   int my_stun = 0;
   if (my_hit) {
     const AttackInfo ad = sT.attacks[my_atk];
@@ -881,12 +871,16 @@ __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k,
     my_stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
   }
   if (!my_hit && my_prox && f.in_back) f.prox = true;  // NotifyInProximityGuardRange (F:400-406)
-  const uint32_t other = xpair((uint32_t)my_hit | ((uint32_t)my_stun << 1));  // the partner's outcome
-  const bool hitB = k == 0 ? my_hit : (other & 1u) != 0;
-  const int stunA = k == 1 ? my_stun : (int)(other >> 1);
-  const int stunB = k == 0 ? my_stun : (int)(other >> 1);
-  if (k == 1 && hitB) f.hits++;  // NotifyAttackHit for P2
-  f.stun = hitB ? stunB : (hitA ? stunA : f.stun);  // SetHitStun on both, phase B last (BC:576-578)
+  // (hit, stun) of both defenders: pA = P2's (phase A), pB = P1's (phase B)
+  const uint32_t mine = (uint32_t)my_hit | ((uint32_t)my_stun << 1);
+  const uint32_t other = xpair(mine);
+  const uint32_t pA = k == 1 ? mine : other, pB = k == 1 ? other : mine;
+  f.hits += k == 1 ? (int)(pB & 1u) : 0;  // NotifyAttackHit for P2
+  // SetHitStun on both, phase B last (BC:576-578), as bit-mask selects (v_bfe_i32 + v_bfi_b32:
+  // written as ?: the compiler branches here)
+  const uint32_t mA = bit0_mask(pA), mB = bit0_mask(pB);
+  const uint32_t sA = (mA & (pA >> 1)) | (~mA & (uint32_t)f.stun);
+  f.stun = (int)((mB & (pB >> 1)) | (~mB & sA));
 }
 
 // KO tick -> End (winner), End tick (BC:221-243, 306-325, 371-381), reduced to
