@@ -424,16 +424,16 @@ __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
 }
 
 // UpdatePushCharacterVsBackground (BC:503-519) with BoxBase semantics
+// Branch-free: with no push the shift is -0.0, the exact identity of IEEE addition (x + -0.0 == x
+// bit for bit, -0.0 included), so every lane applies it.
 template <int FM>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
   const float w = f.pw;
-  const float xmin = bb_xmin<FM>(f.px, w);
-  if (xmin < -kStageHalf) {
-    apply_position_change<FM>(f, fsub<FM>(-kStageHalf, xmin));
-  } else {
-    const float xmax = bb_xmax<FM>(f.px, w);
-    if (xmax > kStageHalf) apply_position_change<FM>(f, fsub<FM>(kStageHalf, xmax));
-  }
+  const float xmin = bb_xmin<FM>(f.px, w), xmax = bb_xmax<FM>(f.px, w);
+  float d_lo = fsub<FM>(-kStageHalf, xmin), d_hi = fsub<FM>(kStageHalf, xmax);
+  asm volatile("" : "+v"(d_lo), "+v"(d_hi));  // both computed: selects, not a branch
+  const float dx = xmin < -kStageHalf ? d_lo : (xmax > kStageHalf ? d_hi : -0.0f);
+  apply_position_change<FM>(f, dx);
 }
 
 // BoxBase (F:8-26): boxes are (world x, width/2, yMin, yMax); xMin = x - w/2, xMax = x + w/2
@@ -1062,25 +1062,27 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   // frame record) instead of being sunk into the collision's branch
   asm volatile("" ::"v"(my_hurt0), "v"(my_hurt1), "v"(their_hit0), "v"(their_hit1), "v"(ym));
   hitbox_hurtbox_collision<FM>(L.f, k, my_hurt0, my_hurt1, their_hit0, their_hit1, (uint32_t)o_rec, ym);
-  // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes
-  const uint32_t mine = (uint32_t)L.f.vital | ((uint32_t)L.f.guard << 2) | ((uint32_t)guard_before << 4);
-  const uint32_t theirs = xpair(mine);
-  const uint32_t w1 = k == 0 ? mine : theirs, w2 = k == 0 ? theirs : mine;
-  const int v1 = w1 & 3, v2 = w2 & 3;
-  const bool over = v1 <= 0 || v2 <= 0;
+  // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes: each
+  // lane's flags (bit 0: vital 0, bit 1: guard dropped this tick; both fields are 0..3) cross
+  // the pair once, then fl1 / fl2 are P1's / P2's
+  const uint32_t my_fl = ((uint32_t)(L.f.vital - 1) >> 31) | (((uint32_t)(L.f.guard - guard_before) >> 31) << 1);
+  const uint32_t o_fl = xpair(my_fl);
+  const uint32_t any_fl = my_fl | o_fl;
+  const bool over = (any_fl & 1u) != 0;
   double reward = 0.0;
   if (p.dense_reward) {
     // Only a guard drop or the round's end moves the f64 sums: on other ticks the reward is
     // 0.0 and `cum += 0.0` is exact (cum starts at +0.0 and a sum of nonzero terms is never -0.0).
-    const bool g1 = ((w1 >> 2) & 3) < (w1 >> 4), g2 = ((w2 >> 2) & 3) < (w2 >> 4);
-    if (g1 | g2 | over) {
-      if (g1) reward -= 0.3;
-      if (g2) reward += 0.3;
+    if (any_fl != 0) {
+      const uint32_t fl1 = k == 0 ? my_fl : o_fl, fl2 = k == 0 ? o_fl : my_fl;
+      if (fl1 & 2u) reward -= 0.3;
+      if (fl2 & 2u) reward += 0.3;
       L.cum += reward;
-      if (over) reward += (double)(v2 == 0 ? 1 : -1) - L.cum;
+      if (over) reward += (double)((fl2 & 1u) ? 1 : -1) - L.cum;
     }
   } else {
-    reward = over ? (v2 == 0 ? 1.0 : -1.0) : 0.0;
+    const uint32_t fl2 = k == 0 ? o_fl : my_fl;
+    reward = over ? ((fl2 & 1u) ? 1.0 : -1.0) : 0.0;
   }
   settle(next);
   if (over) {
