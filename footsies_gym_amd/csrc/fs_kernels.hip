@@ -11,11 +11,13 @@
 // ActionInfo (frame count, loop, cancel window), per (action, frame) an index into
 // 53 de-duplicated 96-B frame records holding every box's geometry, the velocity and
 // the hitbox attack bits -- the window scans of ActionData.cs:87-168 resolved offline
-// (tools/gen_tables.py) -- and the request chain's outcome per (action, window state,
-// inputs).  A tick's dependent LDS round trips: action info, then the record index and
-// the request-table entry together, then the record.  The 180-deep input histories (Fighter.cs:98-101) are two 16-frame
-// shift registers (backward / forward relative to the fighter's facing) plus a
-// saturating attack-hold counter: the reference
+// (tools/gen_tables.py) -- the request chain's outcome per (action, window state, inputs),
+// the box-pair y overlaps per record pair and the hit resolution per (attacker record,
+// overlap mask).  A tick's dependent LDS round trips: action info (read at the end of the
+// previous tick), then the record index and the request-table entry together, then the
+// record with the y-overlap entry, then the resolution entry.  The 180-deep input histories
+// (Fighter.cs:98-101) are two 16-frame shift registers (backward / forward relative to the
+// fighter's facing) plus a saturating attack-hold counter: the reference
 // only reads input[0..16] for dashes (Fighter.cs:585-635, dashAllowFrame 9) and
 // "attack held on input[1..59]" for the charge special (Fighter.cs:569-583).
 //
