@@ -100,6 +100,31 @@ def test_lockstep_from_random_loaded_states(oracle_lib, p2):
     run_lockstep(sim, ora, 200, np.random.default_rng(78), state_every=10, sticky=0.6)
 
 
+# stage edges (±5), outside them, ±0.0 and the smallest denormals: the stage push applies -0.0
+# (the exact identity of IEEE addition) when it does not push, and the character push's tie rule
+EDGE_X = np.array([-0.0, 0.0, 1e-45, -1e-45, 0.3, -0.3, 4.5, -4.5, 4.99, -4.99, 5.0, -5.0, 5.5, -5.5, 7.0, -7.0],
+                  dtype=np.float32)
+
+
+@pytest.mark.parametrize("fm", ["strict", "double"])
+def test_lockstep_edge_positions(oracle_lib, fm):
+    """Loaded states with both fighters on edge positions (and 10 % of arenas on the same x),
+    stepped in lockstep: positions and every other output bit-exact, ±0.0 included."""
+    n = 2048
+    sim, ora = make_pair(oracle_lib, n, "external", fm=fm, seed=31)
+    rng = np.random.default_rng(91)
+    st = random_states(n, rng)
+    for k in range(2):
+        st["f"][:, k]["position_x"] = rng.choice(EDGE_X, n)
+    tie = rng.random(n) < 0.1
+    st["f"][:, 1]["position_x"] = np.where(tie, st["f"][:, 0]["position_x"], st["f"][:, 1]["position_x"])
+    assert np.signbit(st["f"]["position_x"]).any() and (st["f"]["position_x"] == 0).any()
+    assert ora.set_state(st) == 0
+    sim.set_state(st)
+    compare_states(ora.state(), sim.get_state(), step=-1)
+    run_lockstep(sim, ora, 120, np.random.default_rng(92), state_every=5, sticky=0.5)
+
+
 @pytest.mark.parametrize("n_envs,ticks,p2", [(65536, 500, "external"), (262144, 200, "bot"), (262144, 200, "external")])
 def test_full_size_fused_matches_oracle(oracle_lib, n_envs, ticks, p2):
     """BASELINE sizes (C3: 65 536 arenas; C4: 262 144 = 8 x 32 768 on one GPU): the fused kernel
