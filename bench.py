@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-samples", type=int, default=50, help="launches timed back-to-back for roofline")
     ap.add_argument("--no-extras", action="store_true", help="skip the C2 bot-opponent and C5 policy-loop rates")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -235,11 +237,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; the modulo only matters when ranks are rehearsed on fewer devices
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo reduces host tensors
 
     from footsies_gym_amd import _abi
     from footsies_gym_amd._lib import check, lib
@@ -293,7 +301,7 @@ def main():
         torch.cuda.synchronize(dev)
         barrier()
         wall = time.perf_counter() - t0
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64, device=coll_dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item()), ev0.elapsed_time(ev1) / 1e3
@@ -352,7 +360,7 @@ def main():
             rc = rc or fs_pack(h, C.c_void_p(rec.data_ptr()))
             if rc:
                 check(rc, h)
-            if world > 1:
+            if world > 1 and args.dist_backend == "nccl":
                 dist.all_gather_into_tensor(gbuf, rec)
     gwall, _ = timed(run_step_gather, W, kg)
     # dominant kernel of the reported mode, back-to-back launches
@@ -396,7 +404,7 @@ def main():
         "step_gather_mode": {"value": world * N * kg / gwall, "ms_per_step": 1e3 * gwall / kg, "steps": kg,
                              "bytes_gathered_per_step": world * N * _abi.FS_RECORD_BYTES,
                              "note": "fs_step + fs_pack_outputs + one all_gather_into_tensor of the 40-B "
-                                     "(obs, reward, done) records over RCCL per step (none at 1 GPU)"},
+                                     "(obs, reward, done) records over RCCL per step (none at 1 GPU or with --dist-backend gloo)"},
     }
     if world == 1 and not args.no_extras:
         out["p2_bot_mode"] = bot_mode_rate(torch, N, K, W, chunk, args.seed, local)
