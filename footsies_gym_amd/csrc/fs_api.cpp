@@ -528,7 +528,10 @@ FS_API int fs_set_state(fs_handle h, const fs_arena_state* host_in) {
     if (h->cfg.p2_mode == FS_P2_BOT &&
         (s.move_plan < -1 || s.move_plan > 6 || s.attack_plan < -1 || s.attack_plan > 4 || s.move_index < 0 ||
          s.move_index > 127 || s.attack_index < 0 || s.attack_index > 127 ||
-         !valid_action_id(s.prev_opponent_action)))
+         !valid_action_id(s.prev_opponent_action) ||
+         // a queue index lies inside its plan (an index at the end is an empty queue: plan -1)
+         (s.move_plan >= 0 && (uint32_t)s.move_index >= fsk::move_plan_len((uint32_t)s.move_plan)) ||
+         (s.attack_plan >= 0 && (uint32_t)s.attack_index >= fsk::attack_plan_len((uint32_t)s.attack_plan))))
       return set_err(h, FS_E_INVALID, "fs_set_state: arena %d bot state out of range", i);
   }
   int rc;

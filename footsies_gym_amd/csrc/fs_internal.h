@@ -8,6 +8,19 @@
 
 namespace fsk {
 
+// BattleAI's input plans (AI:192-312): the queue of a plan holds plan_len inputs, so a queue
+// index is always below its plan's length (host validation and the kernels' code tables).
+enum { MP_NEUTRAL, MP_FAR1, MP_FAR2, MP_MID1, MP_MID2, MP_FALLBACK1, MP_FALLBACK2 };
+enum { AP_NONE, AP_ONE_HIT, AP_TWO_HIT, AP_IMMEDIATE_SPECIAL, AP_DELAY_SPECIAL };
+constexpr uint32_t move_plan_len(uint32_t plan) {  // AI:192-253
+  return plan == MP_FAR1 ? 90u : plan == MP_FAR2 ? 56u : plan == MP_MID1 ? 70u : plan == MP_MID2 ? 33u
+       : plan == MP_FALLBACK1 ? 60u : plan == MP_FALLBACK2 ? 63u : 30u;
+}
+constexpr uint32_t attack_plan_len(uint32_t plan) {  // AI:255-312
+  return plan == AP_ONE_HIT ? 19u : plan == AP_TWO_HIT ? 23u : plan == AP_IMMEDIATE_SPECIAL ? 61u
+       : plan == AP_DELAY_SPECIAL ? 121u : 30u;
+}
+
 // Per-arena state in HBM, struct-of-arrays (one element per arena, 8/16-byte
 // vectors so one wave64 load/store moves 512 B / 1 KiB contiguous).
 struct DevState {

@@ -501,16 +501,7 @@ __device__ __forceinline__ uint32_t box_x_overlaps(Box4 h0, Box4 h1, float hx0, 
 // ---------------------------------------------------------------------------
 // bot: BattleAI for P2 (AI:10-403) with queues as (plan, index)
 // ---------------------------------------------------------------------------
-enum { MP_NEUTRAL, MP_FAR1, MP_FAR2, MP_MID1, MP_MID2, MP_FALLBACK1, MP_FALLBACK2 };
-enum { AP_NONE, AP_ONE_HIT, AP_TWO_HIT, AP_IMMEDIATE_SPECIAL, AP_DELAY_SPECIAL };
-constexpr uint32_t move_plan_len(uint32_t plan) {  // AI:192-253
-  return plan == MP_FAR1 ? 90u : plan == MP_FAR2 ? 56u : plan == MP_MID1 ? 70u : plan == MP_MID2 ? 33u
-       : plan == MP_FALLBACK1 ? 60u : plan == MP_FALLBACK2 ? 63u : 30u;
-}
-constexpr uint32_t attack_plan_len(uint32_t plan) {  // AI:255-312
-  return plan == AP_ONE_HIT ? 19u : plan == AP_TWO_HIT ? 23u : plan == AP_IMMEDIATE_SPECIAL ? 61u
-       : plan == AP_DELAY_SPECIAL ? 121u : 30u;
-}
+// (the plan enums and lengths are in fs_internal.h: fs_set_state validates queue indices with them)
 
 __device__ __forceinline__ uint32_t rng_next(uint4& s) {  // UnityEngine.Random Xorshift128
   const uint32_t t = s.x ^ (s.x << 11);

@@ -262,7 +262,9 @@ int fs_bind_outputs(fs_handle h, const fs_outputs* dev);
 int fs_get_env_state(fs_handle h, fs_env_state* host_out);
 int fs_get_state(fs_handle h, fs_arena_state* host_out);
 /* Load canonical state [N] from host (STATE_LOAD, BC:153-156, 676-683).
- * Input history beyond what fs_arena_state carries is not representable. */
+ * Input history beyond what fs_arena_state carries is not representable.
+ * FS_E_INVALID (nothing loaded) for a field outside the packed layout's range, or, with the
+ * bot as P2, a queue index at or past its plan's length (such a queue is empty: plan -1). */
 int fs_set_state(fs_handle h, const fs_arena_state* host_in);
 
 /* Block until all work on the handle's stream is done. */

@@ -285,6 +285,27 @@ def test_hashed_actions_match_host_stream(oracle_lib):
     compare_states(ora.state(), s2.get_state())
 
 
+def test_set_state_rejects_queue_index_past_its_plan():
+    """A bot queue index at or past its plan's length is no state the bot can be in (the queue
+    would be empty, exported as plan -1): fs_set_state rejects it, accepts the last input."""
+    from footsies_gym_amd._lib import FootsiesError
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(4, p2_mode="bot", seed=0)
+    st = sim.get_state()
+    for plan_key, idx_key, plan, length in (("move_plan", "move_index", 2, 56),
+                                            ("attack_plan", "attack_index", 4, 121)):
+        bad = st.copy()
+        bad[plan_key][1], bad[idx_key][1] = plan, length
+        with pytest.raises(FootsiesError):
+            sim.set_state(bad)
+        ok = st.copy()
+        ok[plan_key][1], ok[idx_key][1] = plan, length - 1
+        sim.set_state(ok)
+        got = sim.get_state()
+        assert got[plan_key][1] == plan and got[idx_key][1] == length - 1
+    sim.close()
+
+
 @pytest.mark.parametrize("p2", ["bot", "external"])
 def test_state_save_load_roundtrip(oracle_lib, p2):
     """fs_get_state -> fs_set_state into a fresh handle continues bit-identically."""
