@@ -36,9 +36,8 @@ STEP_IO_BYTES = 40      # per env-step: 2 B actions in + 38 B outputs out (inclu
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 10 000 timed ticks = 10 fused launches: SURVEY 8(d)'s C3 protocol (5 runs of 2 000 steps)
-    # as one timed region, so the fixed host cost of the first launch is amortised the same way
-    ap.add_argument("--steps", type=int, default=10000)
+    # SURVEY 8(d)'s C3 protocol: 200 warm-up steps, then 5 timed runs of 2 000 steps (median)
+    ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="arenas per GPU (weak scaling)")
     ap.add_argument("--global-envs", type=int, default=0,
@@ -50,6 +49,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-samples", type=int, default=50, help="launches timed back-to-back for roofline")
+    ap.add_argument("--regions", type=int, default=5,
+                    help="timed regions of exactly --steps steps each, back to back; value = the median region")
+    ap.add_argument("--roofline-ticks", type=int, default=1000,
+                    help="ticks per fs_step_n launch of the roofline block (the shape profiles/ covers)")
     ap.add_argument("--no-extras", action="store_true", help="skip the C2 bot-opponent and C5 policy-loop rates")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -186,6 +189,45 @@ def ppo_rate(torch, N, device, horizon=128, iterations=3):
                       "updates of the 8-64-64-8 actor and critic), P2 = bot" % (N, horizon)}
 
 
+def vector_env_rate(torch, N, steps, device):
+    """The drop-in surface itself at the C3 size: FootsiesVectorEnv.step with numpy (N,) int
+    actions in and numpy obs / reward / info out (the D2H copy and the dict building of every
+    step included), P2 a callable opponent returning pre-drawn numpy actions; then the same
+    env with output="torch": device actions in, device tensors out (zero-copy)."""
+    import numpy as np
+    from footsies_gym_amd.vector_env import FootsiesVectorEnv
+    rng = np.random.default_rng(0)
+    warm = 5
+    a1 = rng.integers(0, 8, (warm + steps, N)).astype(np.uint8)
+    a2 = rng.integers(0, 8, (warm + steps, N)).astype(np.uint8)
+    out = {}
+    for kind in ("numpy", "torch"):
+        k = [0]
+        if kind == "numpy":
+            acts, opp = a1, (lambda obs, info: a2[k[0]])
+        else:
+            acts = torch.as_tensor(a1, device=torch.device("cuda", device))
+            d2 = torch.as_tensor(a2, device=torch.device("cuda", device))
+            opp = (lambda obs, info: d2[k[0]])
+        env = FootsiesVectorEnv(N, device=device, opponent=opp, output=kind, seed=0)
+        env.reset(seed=0)
+        for j in range(warm):
+            k[0] = j
+            env.step(acts[j])
+        torch.cuda.synchronize(device)
+        t = time.perf_counter()
+        for j in range(warm, warm + steps):
+            k[0] = j
+            env.step(acts[j])
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t
+        env.close()
+        out[kind] = {"value": N * steps / dt, "ms_per_step": 1e3 * dt / steps, "steps": steps}
+    out["config"] = ("FootsiesVectorEnv(%d, opponent=callable).step: numpy actions -> numpy obs/info dicts "
+                     "(D2H + conversion every step), and output='torch' (device tensors in/out)" % N)
+    return out
+
+
 def pmc_traffic(kernel, envs, ticks):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/*_traffic.json, written by tools/summarize_profile.py from separate
@@ -262,51 +304,57 @@ def main():
     sim = FootsiesSim(N, device=local, p2_mode="external", seed=rank * N)
     h = sim.handle
     L = lib()
-    # synthetic inputs resident in HBM before timing
-    p1, p2 = sim.hash_actions(W + K, seed=args.seed, t0=0)
+    # synthetic inputs resident in HBM before timing: W warm-up rows, then R regions of K rows
+    R = max(1, args.regions)
+    p1, p2 = sim.hash_actions(W + R * K, seed=args.seed, t0=0)
     torch.cuda.synchronize(dev)
-    base1, base2 = p1.data_ptr(), p2.data_ptr()
     chunk = max(1, min(args.chunk, K))
-    traj = sim.alloc_trajectory(chunk)
-    tdesc = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+    traj = sim.alloc_trajectory(chunk)  # zero-filled: the pages are resident before timing
     fs_step, fs_step_n = L.fs_step, L.fs_step_n
 
-    def run_step(k0, n):
-        for k in range(k0, k0 + n):
-            rc = fs_step(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE)
-            if rc:
-                check(rc, h)
+    def make_runs(a1, a2, tr, ticks_per_launch):
+        b1, b2 = a1.data_ptr(), a2.data_ptr()
+        td = _abi.fs_outputs(**{k: tr[k].data_ptr() for k in _abi.OUTPUT_SPEC})
 
-    def run_fused(k0, n):
-        k = k0
-        while k < k0 + n:
-            m = min(chunk, k0 + n - k)
-            rc = fs_step_n(h, m, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), 0, C.byref(tdesc))
-            if rc:
-                check(rc, h)
-            k += m
+        def run_step(k0, n):
+            for k in range(k0, k0 + n):
+                rc = fs_step(h, C.c_void_p(b1 + k * N), C.c_void_p(b2 + k * N), _abi.FS_ACT_DEVICE)
+                if rc:
+                    check(rc, h)
+
+        def run_fused(k0, n):
+            k = k0
+            while k < k0 + n:
+                m = min(ticks_per_launch, k0 + n - k)
+                rc = fs_step_n(h, m, C.c_void_p(b1 + k * N), C.c_void_p(b2 + k * N), 0, C.byref(td))
+                if rc:
+                    check(rc, h)
+                k += m
+        return run_step, run_fused
+
+    run_step, run_fused = make_runs(p1, p2, traj, chunk)
+    base1, base2 = p1.data_ptr(), p2.data_ptr()
 
     def barrier():
         if world > 1:
             dist.barrier()
 
     def timed(fn, k0, n):
+        """One timed region of exactly n steps: barrier + synchronize on both sides, host
+        wall clock, max over ranks.  Nothing else is issued inside the region."""
         barrier()
         torch.cuda.synchronize(dev)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        ev0.record()
         fn(k0, n)
-        ev1.record()
         torch.cuda.synchronize(dev)
         barrier()
         wall = time.perf_counter() - t0
         t = torch.tensor([wall], dtype=torch.float64, device=coll_dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()), ev0.elapsed_time(ev1) / 1e3
+        return float(t.item())
 
-    def kernel_time(fn, k0, launches, ticks_per_launch):
+    def kernel_time(fn, k0, span, launches, ticks_per_launch):
         """Average kernel duration with the queue pre-filled (a spin kernel holds the GPU while
         the host enqueues), so event pairs bracket back-to-back kernels, not host gaps."""
         torch.cuda.synchronize(dev)
@@ -317,7 +365,7 @@ def main():
             pass
         for j, (a, b) in enumerate(evs):
             a.record()
-            fn(k0 + (j * ticks_per_launch) % max(1, K - ticks_per_launch), ticks_per_launch)
+            fn(k0 + (j * ticks_per_launch) % max(1, span - ticks_per_launch + 1), ticks_per_launch)
             b.record()
         torch.cuda.synchronize(dev)
         d = sorted(a.elapsed_time(b) / 1e3 for a, b in evs)
@@ -328,11 +376,14 @@ def main():
         (run_fused if args.mode == "fused" else run_step)(0, W)
     torch.cuda.synchronize(dev)
 
+    # R back-to-back regions of exactly K steps each (fresh action rows per region); the
+    # median region is reported, every region's wall time is listed
     res = {}
     for mode, fn in (("fused", run_fused), ("step", run_step)):
-        wall, ev = timed(fn, W, K)
-        res[mode] = {"wall_s": wall, "event_s": ev, "env_steps_per_s": world * N * K / wall,
-                     "ms_per_step": 1e3 * wall / K}
+        walls = [timed(fn, W + r * K, K) for r in range(R)]
+        wall = sorted(walls)[len(walls) // 2]
+        res[mode] = {"wall_s": wall, "region_walls_ms": [round(1e3 * w, 4) for w in walls],
+                     "env_steps_per_s": world * N * K / wall, "ms_per_step": 1e3 * wall / K}
     # P1/P2 actions handed over from host memory (FS_ACT_HOST: pinned staging + H2D copy per
     # step), the PCIe-inclusive rate of the per-step path; reported beside, never as `value`
     kh = min(K, 500)
@@ -347,8 +398,7 @@ def main():
     torch.cuda.synchronize(dev)
     host_rate = N * kh / (time.perf_counter() - t0)
     # the per-step path with the multi-GPU exchange of SURVEY 8(e): every step's outputs packed
-    # on device into 40-B records (fs_pack_outputs) and all-gathered over RCCL/xGMI, so every
-    # rank (a centralised learner on rank 0) holds the global batch; reported beside `value`
+    # on device into 40-B records (fs_pack_outputs) and gathered over RCCL/xGMI
     kg = min(K, 500)
     rec = torch.empty((N, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=dev)
     gbuf = torch.empty((world * N, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=dev)
@@ -362,17 +412,35 @@ def main():
                 check(rc, h)
             if world > 1 and args.dist_backend == "nccl":
                 dist.all_gather_into_tensor(gbuf, rec)
-    gwall, _ = timed(run_step_gather, W, kg)
-    # dominant kernel of the reported mode, back-to-back launches
+    gwall = timed(run_step_gather, W, kg)
+    # The dominant kernel of the reported mode, back-to-back launches.  The roofline block is
+    # measured at a fixed launch shape (--roofline-ticks ticks per fs_step_n launch, the shape
+    # the committed rocprofv3 summaries under profiles/ cover), independent of --steps; the
+    # kernel at the timed region's own launch shape is reported beside it.
+    def roofline_at(ticks, fn, span, launches):
+        kt_, kmed_ = kernel_time(fn, W, span, launches, ticks)
+        b = N * (STATE_BYTES + ticks * STEP_IO_BYTES)
+        return kt_, kmed_, b
     if args.mode == "fused":
-        kt, kmed = kernel_time(run_fused, W, max(5, args.kernel_samples // 10), chunk)
-        bytes_per_launch = N * (STATE_BYTES + chunk * STEP_IO_BYTES)
+        rt = max(1, args.roofline_ticks)
+        if rt <= W + R * K and rt == chunk:
+            rfn, rspan = run_fused, W + R * K
+        else:
+            q1, q2 = sim.hash_actions(rt, seed=args.seed ^ 0x5A5A, t0=0)
+            rtraj = traj if rt == chunk else sim.alloc_trajectory(rt)
+            _, rfn = make_runs(q1, q2, rtraj, rt)
+            rspan = rt
+            torch.cuda.synchronize(dev)
+        kt, kmed, bytes_per_launch = roofline_at(rt, rfn, rspan, max(5, args.kernel_samples // 10))
+        ticks = rt
+        st_kt, st_kmed, st_bytes = roofline_at(chunk, run_fused, W + R * K, max(5, args.kernel_samples // 5))
+        kname = "fsk::k_step_n<0, 0>"
     else:
-        kt, kmed = kernel_time(run_step, W, args.kernel_samples, 1)
-        bytes_per_launch = N * (STATE_BYTES + STEP_IO_BYTES)
+        kt, kmed, bytes_per_launch = roofline_at(1, run_step, W + R * K, args.kernel_samples)
+        st_kt, st_kmed, st_bytes = kt, kmed, bytes_per_launch
+        ticks = 1
+        kname = "fsk::k_step<0, 0>"
     achieved = bytes_per_launch / kt / 1e9
-    kname = "fsk::k_step_n<0, 0>" if args.mode == "fused" else "fsk::k_step<0, 0>"
-    ticks = chunk if args.mode == "fused" else 1
     tr = pmc_traffic(kname, N, ticks)
     other = "step" if args.mode == "fused" else "fused"
     out = {
@@ -392,12 +460,21 @@ def main():
                                 "C3: %d arenas/GPU" % N) + ", self-play random actions, P2 external, auto-reset same-step",
                    "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
                    "ticks_per_launch": chunk if args.mode == "fused" else 1, "parallelism": "arena-shard x%d" % world},
+        "timing": {"regions": R, "region_walls_ms": res[args.mode]["region_walls_ms"],
+                   "note": "each region times exactly `steps` steps between barrier + synchronize pairs "
+                           "(host wall clock, max over ranks); value = the median region"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": tr[0] if tr else None,
                      "traffic_source": tr[1] if tr else None,
-                     "kernel": kname, "avg_launch_us": kt * 1e6, "median_launch_us": kmed * 1e6,
-                     "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "kernel": kname, "ticks_per_launch": ticks, "avg_launch_us": kt * 1e6,
+                     "median_launch_us": kmed * 1e6, "algorithmic_bytes_per_launch": bytes_per_launch,
                      "issue": issue_profile(kname, N, ticks)},
+        "kernel_at_timed_shape": {"ticks_per_launch": chunk if args.mode == "fused" else 1,
+                                  "avg_launch_us": st_kt * 1e6, "median_launch_us": st_kmed * 1e6,
+                                  "algorithmic_bytes_per_launch": st_bytes,
+                                  "frac": st_bytes / st_kt / 1e9 / HBM_PEAK_GBPS,
+                                  "traffic": (pmc_traffic(kname, N, chunk if args.mode == "fused" else 1) or
+                                              (None,))[0]},
         other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
         "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
                                    "note": "fs_step with FS_ACT_HOST (PCIe-inclusive action hand-over)"},
@@ -420,6 +497,10 @@ def main():
             out["ppo_end_to_end"] = ppo_rate(torch, N, local)
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             out["ppo_end_to_end"] = {"error": "%s: %s" % (type(e).__name__, e)}
+        try:
+            out["vector_env"] = vector_env_rate(torch, N, min(K, 200), local)
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            out["vector_env"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)
     if rank == 0:
