@@ -6,7 +6,7 @@ the test-side oracle binding (``oracle/binding.py``) agree on layouts.
 """
 import ctypes as C
 
-FS_ABI_VERSION = 1
+FS_ABI_VERSION = 2
 
 FS_OK = 0
 FS_E_INVALID = -1
@@ -17,6 +17,9 @@ FS_E_OOM = -4
 FS_P2_EXTERNAL = 0
 FS_P2_BOT = 1
 FS_P2_NOOP = 2
+
+FS_P1_EXTERNAL = 0
+FS_P1_BOT = 1
 
 FS_FLOAT_STRICT32 = 0
 FS_FLOAT_DOUBLE = 1
@@ -54,7 +57,8 @@ class fs_config(C.Structure):
     _fields_ = [
         ("num_envs", C.c_int32), ("device_id", C.c_int32), ("p2_mode", C.c_int32),
         ("dense_reward", C.c_int32), ("frame_delay", C.c_int32), ("float_mode", C.c_int32),
-        ("autoreset_mode", C.c_int32), ("reserved0", C.c_int32), ("base_seed", C.c_uint64),
+        ("autoreset_mode", C.c_int32), ("p1_mode", C.c_int32), ("base_seed", C.c_uint64),
+        ("arena_base", C.c_uint64),
     ]
 
 
@@ -119,6 +123,9 @@ class fs_arena_state(C.Structure):
         ("rng", C.c_uint32 * 4), ("move_plan", C.c_int32), ("move_index", C.c_int32),
         ("attack_plan", C.c_int32), ("attack_index", C.c_int32), ("prev_distance", C.c_float),
         ("prev_opponent_action", C.c_int32),
+        ("p2_bot", C.c_uint8), ("bot_ready", C.c_uint8 * 2), ("bot_input", C.c_uint8 * 2), ("pad1", C.c_uint8 * 3),
+        ("p1_move_plan", C.c_int32), ("p1_move_index", C.c_int32), ("p1_attack_plan", C.c_int32),
+        ("p1_attack_index", C.c_int32), ("p1_prev_distance", C.c_float), ("p1_prev_opponent_action", C.c_int32),
     ]
 
 
@@ -127,6 +134,7 @@ LIB_FUNCTIONS = {
     "fs_abi_version": (C.c_int, []),
     "fs_create": (C.c_int, [C.POINTER(fs_config), C.POINTER(C.c_void_p)]),
     "fs_reset": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "fs_set_p2_mode": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     "fs_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_masked": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_n": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(fs_outputs)]),

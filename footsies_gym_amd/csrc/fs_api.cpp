@@ -55,6 +55,8 @@ struct fs_context {
   uint8_t* h_mask = nullptr;     // pinned [N]
   hipEvent_t staging_free = nullptr;
   uint4* delay_ring = nullptr;   // frame_delay > 0: [d][N] x 32-B observation records (fs_delay.hip)
+  std::vector<uint8_t> p2bot;    // host mirror of each arena's P2 actor (1 = the bot)
+  int p2bot_count = 0;
   std::vector<void*> allocations;
   uint64_t steps = 0;
   std::string err;
@@ -105,6 +107,18 @@ void free_all(fs_context* h) {
   h->stream = nullptr;
 }
 
+// The kernel variant for the handle's actors (fs_internal.h): the uniform ones unless P1 is the
+// bot or some arena's P2 was switched to the bot.
+int variant(const fs_context* h) {
+  if (h->cfg.p1_mode == FS_P1_BOT || (h->cfg.p2_mode == FS_P2_EXTERNAL && h->p2bot_count > 0)) return fsk::kActors;
+  return h->cfg.p2_mode;
+}
+
+void set_p2bot_mirror(fs_context* h, size_t i, uint8_t bot) {
+  h->p2bot_count += (int)(bot != 0) - (int)(h->p2bot[i] != 0);
+  h->p2bot[i] = bot != 0;
+}
+
 int use_device(fs_context* h) {
   HIP_TRY(h, hipSetDevice(h->device));
   return FS_OK;
@@ -151,6 +165,8 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   if (cfg->num_envs <= 0) return set_err(nullptr, FS_E_INVALID, "num_envs must be > 0 (got %d)", cfg->num_envs);
   if (cfg->p2_mode < FS_P2_EXTERNAL || cfg->p2_mode > FS_P2_NOOP)
     return set_err(nullptr, FS_E_INVALID, "invalid p2_mode %d", cfg->p2_mode);
+  if (cfg->p1_mode != FS_P1_EXTERNAL && cfg->p1_mode != FS_P1_BOT)
+    return set_err(nullptr, FS_E_INVALID, "invalid p1_mode %d", cfg->p1_mode);
   if (cfg->float_mode != FS_FLOAT_STRICT32 && cfg->float_mode != FS_FLOAT_DOUBLE)
     return set_err(nullptr, FS_E_INVALID, "invalid float_mode %d", cfg->float_mode);
   if (cfg->autoreset_mode != FS_AUTORESET_SAME_STEP && cfg->autoreset_mode != FS_AUTORESET_NEXT_STEP)
@@ -171,7 +187,6 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   h->n = cfg->num_envs;
   h->device = cfg->device_id;
   const size_t N = (size_t)h->n;
-  const bool bot = cfg->p2_mode == FS_P2_BOT;
   int rc = FS_OK;
   auto fail = [&](int code) {
     std::string msg = h->err;
@@ -190,7 +205,11 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   if ((rc = dalloc(h, &h->st.pos, N)) || (rc = dalloc(h, &h->st.hist, N)) || (rc = dalloc(h, &h->st.fpk, N)) ||
       (rc = dalloc(h, &h->st.aw, N)) || (rc = dalloc(h, &h->st.cum, N)))
     return fail(rc);
-  if (bot && ((rc = dalloc(h, &h->st.rng, N)) || (rc = dalloc(h, &h->st.bot, N)))) return fail(rc);
+  // the game RNG and both BattleAIs exist in every mode (a P2 bot can be switched in later)
+  if ((rc = dalloc(h, &h->st.rng, N)) || (rc = dalloc(h, &h->st.bot, N)) || (rc = dalloc(h, &h->st.bot1, N)))
+    return fail(rc);
+  h->p2bot.assign(N, cfg->p2_mode == FS_P2_BOT ? 1 : 0);
+  h->p2bot_count = cfg->p2_mode == FS_P2_BOT ? h->n : 0;
   // outputs
   Buffers& b = h->own;
   if ((rc = dalloc(h, &b.guard, 2 * N)) || (rc = dalloc(h, &b.move, 2 * N)) || (rc = dalloc(h, &b.action, 2 * N)) ||
@@ -226,7 +245,10 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   rp.flags = FS_RESET_HARD;
   rp.init = 1;
   rp.base_seed = cfg->base_seed;
-  hipError_t le = fsk::launch_reset(rp, cfg->float_mode, cfg->p2_mode, h->stream);
+  rp.arena_base = cfg->arena_base;
+  rp.p1_bot = cfg->p1_mode == FS_P1_BOT;
+  rp.p2_mode = cfg->p2_mode;
+  hipError_t le = fsk::launch_reset(rp, cfg->float_mode, h->stream);
   if (le != hipSuccess) return fail(set_err(h, FS_E_DEVICE, "reset kernel launch: %s", hipGetErrorString(le)));
   if ((rc = apply_delay(h, h->out, 1, 0, true))) return fail(rc);  // the first reset's queue (FE:502-504)
   le = hipStreamSynchronize(h->stream);
@@ -250,6 +272,9 @@ FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int
   rp.n_envs = h->n;
   rp.flags = flags;
   rp.init = 0;
+  rp.arena_base = h->cfg.arena_base;
+  rp.p1_bot = h->cfg.p1_mode == FS_P1_BOT;
+  rp.p2_mode = h->cfg.p2_mode;
   if (seeds) {
     memcpy(h->h_seeds, seeds, N * sizeof(uint64_t));
     HIP_TRY(h, hipMemcpyAsync(h->d_seeds, h->h_seeds, N * sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
@@ -261,7 +286,7 @@ FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int
     rp.mask = h->d_mask;
   }
   HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
-  HIP_TRY(h, fsk::launch_reset(rp, h->cfg.float_mode, h->cfg.p2_mode, h->stream));
+  HIP_TRY(h, fsk::launch_reset(rp, h->cfg.float_mode, h->stream));
   if (flags != FS_RESET_SEED_ONLY && (rc = apply_delay(h, h->out, 1, 0, true))) return rc;
   return FS_OK;
 }
@@ -282,13 +307,19 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
   sp.autoreset_mode = h->cfg.autoreset_mode;
   sp.action_seed = seed;
   sp.t0 = h->steps;
+  sp.arena_base = h->cfg.arena_base;
+  sp.p1_bot = h->cfg.p1_mode == FS_P1_BOT;
+  sp.p2_resets = h->cfg.p2_mode == FS_P2_BOT;
+  sp.p2_noop = h->cfg.p2_mode == FS_P2_NOOP;
   if (pol) sp.pol = fsk::PolicyParams{pol->w1, pol->b1, pol->w2, pol->b2, pol->w3, pol->b3,
                                       pol->actions_out, pol->logp_out, pol->seed};
   const bool ext = h->cfg.p2_mode == FS_P2_EXTERNAL;
-  if (flags == FS_ACT_HOST && p1) {
+  const bool p1_bot = h->cfg.p1_mode == FS_P1_BOT;
+  if (flags == FS_ACT_HOST && (p1 || p1_bot)) {
     if (n != 1) return set_err(h, FS_E_INVALID, "host actions are only accepted for single steps");
     if ((rc = staging_wait(h))) return rc;
-    memcpy(h->h_act, p1, N);
+    if (p1) memcpy(h->h_act, p1, N);
+    else memset(h->h_act, 0, N);  // P1 is the bot: the row is not read
     if (ext) memcpy(h->h_act + N, p2, N);
     HIP_TRY(h, hipMemcpyAsync(h->d_act, h->h_act, ext ? 2 * N : N, hipMemcpyHostToDevice, h->stream));
     if (active) {
@@ -300,7 +331,9 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
     sp.p2 = ext ? h->d_act + N : nullptr;
     sp.active = active ? h->d_mask : nullptr;
   } else {
-    sp.p1 = p1;
+    // P1 bot with explicit P2 rows: P1's row is never read, but a null p1 would select the
+    // hashed-action kernel, so it points at the staging row
+    sp.p1 = (p1_bot && !p1 && p2) ? h->d_act : p1;
     sp.p2 = ext ? p2 : nullptr;
     sp.active = active;
   }
@@ -325,11 +358,12 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
     for (int j = 0; j < n; j++) {
       const uint8_t* q1 = sp.p1 ? sp.p1 + (size_t)j * N : nullptr;
       const uint8_t* q2 = sp.p2 ? sp.p2 + (size_t)j * N : nullptr;
-      if ((rc = step_common(h, 1, q1, q2, FS_ACT_DEVICE, seed, nullptr))) return rc;
+      if ((rc = step_common(h, 1, q1 ? q1 : (p1_bot ? h->d_act : nullptr), q2, FS_ACT_DEVICE, seed, nullptr)))
+        return rc;
     }
     return FS_OK;
   }
-  HIP_TRY(h, fsk::launch_step(sp, h->cfg.float_mode, h->cfg.p2_mode, h->stream));
+  HIP_TRY(h, fsk::launch_step(sp, h->cfg.float_mode, variant(h), h->stream));
   if ((rc = apply_delay(h, sp.out, n, sp.out_stride_steps, false))) return rc;
   h->steps += (uint64_t)n;
   return FS_OK;
@@ -376,9 +410,33 @@ static int step_chunked(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2
   return FS_OK;
 }
 
+FS_API int fs_set_p2_mode(fs_handle h, int mode, const uint8_t* mask) {
+  if (!h) return FS_E_INVALID;
+  if (mode != FS_P2_EXTERNAL && mode != FS_P2_BOT)
+    return set_err(h, FS_E_INVALID, "fs_set_p2_mode: mode must be FS_P2_EXTERNAL or FS_P2_BOT (got %d)", mode);
+  if (h->cfg.p2_mode != FS_P2_EXTERNAL)
+    return set_err(h, FS_E_UNSUPPORTED, "fs_set_p2_mode: the handle needs a remote P2 (FS_P2_EXTERNAL) to switch "
+                                        "its opponent (FE:468-470)");
+  int rc;
+  if ((rc = use_device(h))) return rc;
+  const size_t N = (size_t)h->n;
+  const uint8_t* dmask = nullptr;
+  if (mask) {
+    if ((rc = staging_wait(h))) return rc;
+    memcpy(h->h_mask, mask, N);
+    HIP_TRY(h, hipMemcpyAsync(h->d_mask, h->h_mask, N, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipEventRecord(h->staging_free, h->stream));
+    dmask = h->d_mask;
+  }
+  HIP_TRY(h, fsk::launch_set_p2(h->st, mode == FS_P2_BOT, dmask, h->n, h->stream));
+  for (size_t i = 0; i < N; i++)
+    if (!mask || mask[i]) set_p2bot_mirror(h, i, mode == FS_P2_BOT);
+  return FS_OK;
+}
+
 FS_API int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags) {
   if (!h) return FS_E_INVALID;
-  if (!p1_act) return set_err(h, FS_E_INVALID, "fs_step: p1 actions required");
+  if (!p1_act && h->cfg.p1_mode != FS_P1_BOT) return set_err(h, FS_E_INVALID, "fs_step: p1 actions required");
   if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
     return set_err(h, FS_E_INVALID, "fs_step: p2 actions required for FS_P2_EXTERNAL");
   if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
@@ -388,7 +446,8 @@ FS_API int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, in
 FS_API int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, const uint8_t* active,
                           int flags) {
   if (!h) return FS_E_INVALID;
-  if (!p1_act || !active) return set_err(h, FS_E_INVALID, "fs_step_masked: p1 actions and mask required");
+  if ((!p1_act && h->cfg.p1_mode != FS_P1_BOT) || !active)
+    return set_err(h, FS_E_INVALID, "fs_step_masked: p1 actions and mask required");
   if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
     return set_err(h, FS_E_INVALID, "fs_step_masked: p2 actions required for FS_P2_EXTERNAL");
   if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
@@ -401,7 +460,8 @@ FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p
                      const fs_outputs* traj) {
   if (!h) return FS_E_INVALID;
   if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n: n must be > 0");
-  if ((p1_act == nullptr) != (p2_act == nullptr) && h->cfg.p2_mode == FS_P2_EXTERNAL)
+  if ((p1_act == nullptr) != (p2_act == nullptr) && h->cfg.p2_mode == FS_P2_EXTERNAL &&
+      !(p1_act == nullptr && h->cfg.p1_mode == FS_P1_BOT))
     return set_err(h, FS_E_INVALID, "fs_step_n: give both action arrays or neither");
   return step_chunked(h, n, p1_act, p2_act, action_seed, traj, nullptr);
 }
@@ -412,6 +472,8 @@ FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint
   if (!pol || !pol->w1 || !pol->b1 || !pol->w2 || !pol->b2 || !pol->w3 || !pol->b3)
     return set_err(h, FS_E_INVALID, "fs_step_n_policy: all six weight arrays required");
   if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n_policy: n must be > 0");
+  if (h->cfg.p1_mode == FS_P1_BOT)
+    return set_err(h, FS_E_UNSUPPORTED, "fs_step_n_policy: P1 is the bot (FS_P1_BOT), not the actor");
   if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
     return set_err(h, FS_E_INVALID, "fs_step_n_policy: p2 actions required for FS_P2_EXTERNAL");
   if (h->cfg.frame_delay > 0)
@@ -424,7 +486,7 @@ FS_API int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0,
   if (!h || !p1_out || n_steps <= 0) return FS_E_INVALID;
   int rc;
   if ((rc = use_device(h))) return rc;
-  HIP_TRY(h, fsk::launch_hash_actions(h->n, n_steps, seed, t0, p1_out, p2_out, h->stream));
+  HIP_TRY(h, fsk::launch_hash_actions(h->n, n_steps, seed, t0, h->cfg.arena_base, p1_out, p2_out, h->stream));
   return FS_OK;
 }
 
@@ -479,7 +541,7 @@ FS_API int fs_get_env_state(fs_handle h, fs_env_state* host_out) {
   if ((rc = use_device(h))) return rc;
   fs_env_state* d = nullptr;
   HIP_TRY(h, hipMalloc(&d, sizeof(fs_env_state) * (size_t)h->n));
-  hipError_t e = fsk::launch_get_state(h->st, nullptr, d, h->n, h->cfg.p2_mode, h->stream);
+  hipError_t e = fsk::launch_get_state(h->st, nullptr, d, h->n, h->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(host_out, d, sizeof(fs_env_state) * (size_t)h->n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -494,7 +556,7 @@ FS_API int fs_get_state(fs_handle h, fs_arena_state* host_out) {
   if ((rc = use_device(h))) return rc;
   fs_arena_state* d = nullptr;
   HIP_TRY(h, hipMalloc(&d, sizeof(fs_arena_state) * (size_t)h->n));
-  hipError_t e = fsk::launch_get_state(h->st, d, nullptr, h->n, h->cfg.p2_mode, h->stream);
+  hipError_t e = fsk::launch_get_state(h->st, d, nullptr, h->n, h->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(host_out, d, sizeof(fs_arena_state) * (size_t)h->n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -508,6 +570,13 @@ static bool valid_action_id(int32_t id) {
   for (int32_t k : kIds)
     if (k == id) return true;
   return false;
+}
+// a BattleAI's canonical fields fit the bot word, and a queue index lies inside its plan (an
+// index at the end is an empty queue: plan -1)
+static bool valid_bot(int32_t mp, int32_t mi, int32_t ap, int32_t ai, int32_t prev_opp) {
+  return mp >= -1 && mp <= 6 && ap >= -1 && ap <= 4 && mi >= 0 && mi <= 127 && ai >= 0 && ai <= 127 &&
+         valid_action_id(prev_opp) && (mp < 0 || (uint32_t)mi < fsk::move_plan_len((uint32_t)mp)) &&
+         (ap < 0 || (uint32_t)ai < fsk::attack_plan_len((uint32_t)ap));
 }
 
 FS_API int fs_set_state(fs_handle h, const fs_arena_state* host_in) {
@@ -525,24 +594,27 @@ FS_API int fs_set_state(fs_handle h, const fs_arena_state* host_in) {
     }
     if (s.recording_count < 0 || s.recording_count > 18000)
       return set_err(h, FS_E_INVALID, "fs_set_state: arena %d recording_count out of range", i);
-    if (h->cfg.p2_mode == FS_P2_BOT &&
-        (s.move_plan < -1 || s.move_plan > 6 || s.attack_plan < -1 || s.attack_plan > 4 || s.move_index < 0 ||
-         s.move_index > 127 || s.attack_index < 0 || s.attack_index > 127 ||
-         !valid_action_id(s.prev_opponent_action) ||
-         // a queue index lies inside its plan (an index at the end is an empty queue: plan -1)
-         (s.move_plan >= 0 && (uint32_t)s.move_index >= fsk::move_plan_len((uint32_t)s.move_plan)) ||
-         (s.attack_plan >= 0 && (uint32_t)s.attack_index >= fsk::attack_plan_len((uint32_t)s.attack_plan))))
+    if (!valid_bot(s.move_plan, s.move_index, s.attack_plan, s.attack_index, s.prev_opponent_action) ||
+        !valid_bot(s.p1_move_plan, s.p1_move_index, s.p1_attack_plan, s.p1_attack_index,
+                   s.p1_prev_opponent_action) ||
+        s.bot_ready[0] > 1 || s.bot_ready[1] > 1 || s.bot_input[0] > 7 || s.bot_input[1] > 7 || s.p2_bot > 1)
       return set_err(h, FS_E_INVALID, "fs_set_state: arena %d bot state out of range", i);
+    // a bot-created P2 is the bot for good and is Reset at every Intro (always ready); an idle P2
+    // has no bot
+    if ((h->cfg.p2_mode == FS_P2_BOT && (!s.p2_bot || !s.bot_ready[1])) ||
+        (h->cfg.p2_mode == FS_P2_NOOP && s.p2_bot))
+      return set_err(h, FS_E_INVALID, "fs_set_state: arena %d p2_bot / bot_ready do not fit the handle's P2 mode", i);
   }
   int rc;
   if ((rc = use_device(h))) return rc;
   fs_arena_state* d = nullptr;
   HIP_TRY(h, hipMalloc(&d, sizeof(fs_arena_state) * (size_t)h->n));
   hipError_t e = hipMemcpyAsync(d, host_in, sizeof(fs_arena_state) * (size_t)h->n, hipMemcpyHostToDevice, h->stream);
-  if (e == hipSuccess) e = fsk::launch_set_state(h->st, d, h->n, h->cfg.p2_mode, h->stream);
+  if (e == hipSuccess) e = fsk::launch_set_state(h->st, d, h->n, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   (void)hipFree(d);
   if (e != hipSuccess) return set_err(h, FS_E_DEVICE, "fs_set_state: %s", hipGetErrorString(e));
+  for (int i = 0; i < h->n; i++) set_p2bot_mirror(h, (size_t)i, host_in[i].p2_bot);
   return FS_OK;
 }
 

@@ -29,9 +29,15 @@ struct DevState {
   uint4* fpk;      // packed fighter words: (P1 lo, P1 hi, P2 lo, P2 hi), layout in fs_kernels.hip
   int2* aw;        // (frameCount, arena header word)
   double* cum;     // FootsiesEnv._cummulative_episode_reward
-  uint4* rng;      // bot: UnityEngine.Random Xorshift128 state
-  uint2* bot;      // bot: (queue word, previous FightState distance bits)
+  uint4* rng;      // the game's UnityEngine.Random Xorshift128 state (every mode)
+  uint2* bot;      // P2's BattleAI: (bot word, previous FightState distance bits), layout in fs_kernels.hip
+  uint2* bot1;     // P1's BattleAI (FS_P1_BOT), same layout
 };
+
+// The kernels' P2 variants.  FS_P2_EXTERNAL / FS_P2_BOT / FS_P2_NOOP run handles whose actors are
+// fixed and uniform (P1 the agent; P2 remote, the bot, or idle); kActors runs per-arena actors: a
+// P1 bot (FS_P1_BOT) and / or P2 switched between remote and bot (fs_set_p2_mode).
+constexpr int kActors = 3;
 
 struct DevOutputs {
   uint8_t* guard;
@@ -70,11 +76,15 @@ struct StepParams {
   const uint8_t* active;  // [N] or null: single-tick launches skip arenas whose byte is 0
   uint64_t action_seed;
   uint64_t t0;         // global step index of the first tick (hash counter)
+  uint64_t arena_base; // global index of arena 0 (fs_config.arena_base): hash / sampling keys
   int n_envs;
   int n_steps;
   int out_stride_steps;  // 1: outputs are [n][N] trajectories; 0: overwrite one [N] set
   int dense_reward;
   int autoreset_mode;
+  int p1_bot;     // kActors: P1 is the bot (FS_P1_BOT)
+  int p2_resets;  // kActors: P2's bot is Reset at Intro (the handle was created with FS_P2_BOT)
+  int p2_noop;    // kActors: a non-bot P2 presses nothing (FS_P2_NOOP handle)
 };
 
 struct ResetParams {
@@ -86,6 +96,8 @@ struct ResetParams {
   int flags;
   int init;  // 1: fresh arenas (`new Fighter()`), seeds from base_seed
   uint64_t base_seed;
+  uint64_t arena_base;
+  int p1_bot, p2_mode;  // the handle's actors (fs_config p1_mode / p2_mode)
 };
 
 // FootsiesEnv's delayed-frame queue (FE:126-131, 493-504, 532-535) for frame_delay = d > 0:
@@ -105,13 +117,14 @@ struct DelayParams {
 };
 
 // launchers (fs_kernels.hip, fs_delay.hip); return hipError_t of the launch
-hipError_t launch_step(const StepParams& p, int float_mode, int p2_mode, hipStream_t s);
-hipError_t launch_reset(const ResetParams& p, int float_mode, int p2_mode, hipStream_t s);
-hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1, uint8_t* p2,
-                               hipStream_t s);
-hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_state* env_dst, int n, int p2_mode,
-                            hipStream_t s);
-hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, int p2_mode, hipStream_t s);
+// variant: FS_P2_EXTERNAL / FS_P2_BOT / FS_P2_NOOP or kActors (see above)
+hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStream_t s);
+hipError_t launch_reset(const ResetParams& p, int float_mode, hipStream_t s);
+hipError_t launch_set_p2(const DevState& st, int bot, const uint8_t* mask, int n, hipStream_t s);
+hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint64_t arena_base, uint8_t* p1,
+                               uint8_t* p2, hipStream_t s);
+hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_state* env_dst, int n, hipStream_t s);
+hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, hipStream_t s);
 hipError_t launch_delay(const DelayParams& p, hipStream_t s);
 hipError_t launch_pack_records(const DevOutputs& o, void* dst, int n, hipStream_t s);
 

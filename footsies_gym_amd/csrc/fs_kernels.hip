@@ -56,11 +56,12 @@ constexpr int kBlock = 256;
 //   [21,23) guard | [23,25) hit count | [25,30) buffer idx | [30,35) reserve idx |
 //   35 isInputBackward | 36 isReserveProximityGuard | 37 hasWon | [38,44) attack hold
 // arena header word (DevState::aw.y)
-//   [0,15) recording count | [15,18) rec P1 | [18,21) rec P2 | [21,24) actor P1 |
-//   [24,27) actor P2 | 27 reset pending | 28 has_terminated
-// bot word (DevState::bot.x)
+//   [0,15) recording count | [15,18) rec P1 | [18,21) rec P2 | [21,24) remote actor P1 input |
+//   [24,27) remote actor P2 input | 27 reset pending | 28 has_terminated | 29 P2's actor is the bot
+// bot word (DevState::bot.x for P2's BattleAI, DevState::bot1.x for P1's)
 //   [0,3) move plan+1 (0 = empty) | [3,10) move index | [10,13) attack plan+1 |
-//   [13,20) attack index | [20,25) previous FightState opponent action idx
+//   [13,20) attack index | [20,25) previous FightState opponent action idx |
+//   25 ready (fightStates[5] set) | [26,29) the bot actor's last input (TrainingBattleAIActor.input)
 // ---------------------------------------------------------------------------
 
 struct Fighter {
@@ -82,8 +83,8 @@ struct Arena {
   bool pending, has_term;
   double cum;
   uint4 rng;
-  uint32_t mplan, midx, aplan, aidx, prev_opp;
-  float prev_dist;
+  bool p2bot;
+  uint2 bw[2];  // bot words of P1's and P2's BattleAI (decoded by the state kernels)
 };
 
 __device__ __forceinline__ void unpack_fighter(Fighter& f, uint32_t lo, uint32_t hi) {
@@ -109,7 +110,6 @@ __device__ __forceinline__ uint64_t pack_fighter(const Fighter& f) {
          ((uint64_t)f.won << 37) | ((uint64_t)f.hold << 38);
 }
 
-template <bool BOT>
 __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
   float2 pos = s.pos[i];
   uint2 hist = s.hist[i];
@@ -131,33 +131,24 @@ __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
   A.act2 = (h >> 24) & 7;
   A.pending = (h >> 27) & 1;
   A.has_term = (h >> 28) & 1;
-  if constexpr (BOT) {
-    A.rng = s.rng[i];
-    uint2 b = s.bot[i];
-    A.mplan = b.x & 7;
-    A.midx = (b.x >> 3) & 127;
-    A.aplan = (b.x >> 10) & 7;
-    A.aidx = (b.x >> 13) & 127;
-    A.prev_opp = (b.x >> 20) & 31;
-    A.prev_dist = __uint_as_float(b.y);
-  }
+  A.p2bot = (h >> 29) & 1;
+  A.rng = s.rng[i];
+  A.bw[0] = s.bot1[i];
+  A.bw[1] = s.bot[i];
 }
 
-template <bool BOT>
 __device__ __forceinline__ void store_arena(const Arena& A, const DevState& s, int i) {
   uint64_t w0 = pack_fighter(A.f0), w1 = pack_fighter(A.f1);
   s.pos[i] = make_float2(A.f0.x, A.f1.x);
   s.hist[i] = make_uint2(A.f0.hist, A.f1.hist);
   s.fpk[i] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   uint32_t h = A.rec_count | (A.rec1 << 15) | (A.rec2 << 18) | (A.act1 << 21) | (A.act2 << 24) |
-               ((uint32_t)A.pending << 27) | ((uint32_t)A.has_term << 28);
+               ((uint32_t)A.pending << 27) | ((uint32_t)A.has_term << 28) | ((uint32_t)A.p2bot << 29);
   s.aw[i] = make_int2(A.frame_count, (int)h);
   s.cum[i] = A.cum;
-  if constexpr (BOT) {
-    s.rng[i] = A.rng;
-    s.bot[i] = make_uint2(A.mplan | (A.midx << 3) | (A.aplan << 10) | (A.aidx << 13) | (A.prev_opp << 20),
-                          __float_as_uint(A.prev_dist));
-  }
+  s.rng[i] = A.rng;
+  s.bot1[i] = A.bw[0];
+  s.bot[i] = A.bw[1];
 }
 
 // ---------------------------------------------------------------------------
@@ -708,6 +699,84 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dis
   return mine | xpair(mine);
 }
 
+// The whole BattleAI of one fighter on one lane (both queues), for the per-arena actor variant
+// (kActors): P1's bot (by_example) on the P1 lane, P2's on the P2 lane, the game's one RNG passed
+// between them in TrainingManager.Step's order (P1 first).  Off the throughput path, so written
+// with plain branches.
+struct FullBot {
+  uint32_t mplan, midx, aplan, aidx;  // plans stored + 1 (0 = empty queue)
+  uint32_t prev_opp;                  // fightStates[5]: opponent action idx ...
+  float prev_dist;                    // ... and distance
+  bool ready;                         // fightStates[5] != null
+};
+
+__device__ __forceinline__ FullBot unpack_bot(uint2 w, uint32_t& input) {
+  FullBot b;
+  b.mplan = w.x & 7;
+  b.midx = (w.x >> 3) & 127;
+  b.aplan = (w.x >> 10) & 7;
+  b.aidx = (w.x >> 13) & 127;
+  b.prev_opp = (w.x >> 20) & 31;
+  b.ready = (w.x >> 25) & 1;
+  input = (w.x >> 26) & 7;
+  b.prev_dist = __uint_as_float(w.y);
+  return b;
+}
+__device__ __forceinline__ uint2 pack_bot(const FullBot& b, uint32_t input) {
+  return make_uint2(b.mplan | (b.midx << 3) | (b.aplan << 10) | (b.aidx << 13) | (b.prev_opp << 20) |
+                        ((uint32_t)b.ready << 25) | (input << 26),
+                    __float_as_uint(b.prev_dist));
+}
+
+// getNextAIInput (AI:41-66) of fighter k's bot: UpdateFightState (AI:344-363) first, then the
+// previous call's state decides; a bot whose fightStates[5] is still null (never Reset, first
+// call) answers 0 without touching its queues or the RNG.  P1's forward is Right (AI:380-388),
+// so its movement codes are mirrored.
+__device__ __forceinline__ uint32_t bot_full_next(FullBot& b, uint4& rng, uint32_t k, float dist, uint32_t opp_act) {
+  const bool ready = b.ready;
+  const float d = b.prev_dist;
+  const uint32_t opp = b.prev_opp;
+  b.prev_dist = dist;
+  b.prev_opp = opp_act;
+  b.ready = true;
+  if (!ready) return 0u;
+  const uint32_t bucket = d > 4.0f ? 0u : d > 3.0f ? 1u : d > 2.5f ? 2u : d > 2.0f ? 3u : 4u;
+  uint32_t in = 0;
+  if (b.mplan != 0) {  // moveQueue.Dequeue
+    const uint32_t p = b.mplan - 1, i = b.midx;
+    const uint32_t c = (sBot.codes[1][p][i >> 4] >> (2 * (i & 15))) & 3u;
+    in |= k == 0 ? (((c & 1u) << 1) | (c >> 1)) : c;
+    b.midx = i + 1;
+    if (b.midx == sBot.len[1][p]) b.mplan = 0;
+  } else {  // SelectMovement (AI:68-126)
+    const BotDraw w = sBot.draw[1][bucket];
+    b.mplan = ((w.map >> (4 * draw_mod(rng_next(rng), w))) & 15u) + 1;
+    b.midx = 0;
+  }
+  if (b.aplan != 0) {  // attackQueue.Dequeue
+    const uint32_t p = b.aplan - 1, i = b.aidx;
+    in |= ((sBot.codes[0][p][i >> 4] >> (2 * (i & 15))) & 1u) << 2;
+    b.aidx = i + 1;
+    if (b.aidx == sBot.len[0][p]) b.aplan = 0;
+  } else if (attack_forced(bucket, opp)) {  // SelectAttack without a draw (AI:130-133, 147-151)
+    b.aplan = AP_TWO_HIT + 1;
+    b.aidx = 0;
+  } else {  // SelectAttack (AI:128-190)
+    const BotDraw w = sBot.draw[0][bucket];
+    b.aplan = ((w.map >> (4 * draw_mod(rng_next(rng), w))) & 15u) + 1;
+    b.aidx = 0;
+  }
+  return in;
+}
+
+// BattleAI.Reset (AI:393-403): empty queues, every FightState slot = the current state
+__device__ __forceinline__ void bot_full_reset(FullBot& b, float dist, uint32_t opp_act) {
+  b.mplan = b.midx = b.aplan = b.aidx = 0;
+  b.prev_dist = dist;
+  b.prev_opp = opp_act;
+  b.ready = true;
+}
+
 // ---------------------------------------------------------------------------
 // Two lanes per arena.  Lane 2a+k runs fighter k of arena a (k = 0: P1, faces
 // right; k = 1: P2).  Per-fighter phases (UpdateInput .. UpdateBoxes) run on
@@ -732,12 +801,16 @@ struct Lane {
   bool pending, has_term;
   double cum;
   uint32_t rec;       // this player's recordingPnInput[index - 1]
-  uint32_t act;       // this player's TrainingActor.GetInput()
+  uint32_t act;       // this player's remote actor's input (TrainingRemoteActor.input)
+  uint32_t bin;       // this player's bot actor's input (TrainingBattleAIActor.input), bot lanes only
+  bool p2bot;         // kActors: P2's actor is the bot (replica)
   AInfo ai;           // ActionInfo of f.act (reloaded at the end of every tick)
   Bot bot;            // FS_P2_BOT only: this lane's queue + replicas (see Bot)
+  FullBot fb;         // kActors only: this fighter's whole BattleAI
+  uint4 rng;          // kActors only: the game's RNG (replica)
 };
 
-template <bool BOT>
+template <int V>
 __device__ __forceinline__ void load_lane(Lane& L, const DevState& s, int a, uint32_t k) {
   const int l = 2 * a + (int)k;
   L.k = k;
@@ -754,17 +827,23 @@ __device__ __forceinline__ void load_lane(Lane& L, const DevState& s, int a, uin
   L.act = (h >> (k ? 24 : 21)) & 7;
   L.pending = (h >> 27) & 1;
   L.has_term = (h >> 28) & 1;
-  if constexpr (BOT) {  // both lanes read the same 24 B (one cache line); P2 uses it
+  L.p2bot = (h >> 29) & 1;
+  L.bin = 0;
+  if constexpr (V == FS_P2_BOT) {  // both lanes read the same 24 B (one cache line); P2 uses it
     L.bot.rng = s.rng[a];
     const uint2 b = s.bot[a];
     L.bot.plan = k ? (b.x & 7) : ((b.x >> 10) & 7);  // P2 lane: movement queue, P1 lane: attack queue
     L.bot.idx = k ? ((b.x >> 3) & 127) : ((b.x >> 13) & 127);
     L.bot.prev_opp = (b.x >> 20) & 31;
     L.bot.prev_dist = __uint_as_float(b.y);
+    L.bin = (b.x >> 26) & 7;  // (a bot-created P2 is Reset at every Intro: always ready)
+  } else if constexpr (V == kActors) {
+    L.rng = s.rng[a];
+    L.fb = unpack_bot(k ? s.bot[a] : s.bot1[a], L.bin);
   }
 }
 
-template <bool BOT>
+template <int V>
 __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int a) {
   const int l = 2 * a + (int)L.k;
   const uint64_t w = pack_fighter(L.f);
@@ -773,17 +852,27 @@ __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int
   reinterpret_cast<uint2*>(s.fpk)[l] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
   const uint32_t other = xpair(L.rec | (L.act << 3));  // P2's recorded/actor input for the header
   if (L.k == 0) {
+    const uint32_t p2bot = V == FS_P2_BOT ? 1u : V == kActors ? (uint32_t)L.p2bot : 0u;
     const uint32_t h = L.rec_count | (L.rec << 15) | ((other & 7) << 18) | (L.act << 21) | ((other >> 3) << 24) |
-                       ((uint32_t)L.pending << 27) | ((uint32_t)L.has_term << 28);
+                       ((uint32_t)L.pending << 27) | ((uint32_t)L.has_term << 28) | (p2bot << 29);
     s.aw[a] = make_int2(L.frame_count, (int)h);
     s.cum[a] = L.cum;
   }
-  if constexpr (BOT) {
+  if constexpr (V == FS_P2_BOT) {
     const Bot& b = L.bot;
     const uint32_t mine = b.plan | (b.idx << 3), other = xpair(mine);  // the partner's queue
     if (L.k == 1) {
       s.rng[a] = b.rng;
-      s.bot[a] = make_uint2(mine | (other << 10) | (b.prev_opp << 20), __float_as_uint(b.prev_dist));
+      s.bot[a] = make_uint2(mine | (other << 10) | (b.prev_opp << 20) | (1u << 25) | (L.bin << 26),
+                            __float_as_uint(b.prev_dist));
+    }
+  } else if constexpr (V == kActors) {
+    const uint2 bw = pack_bot(L.fb, L.bin);
+    if (L.k == 1) {
+      s.rng[a] = L.rng;
+      s.bot[a] = bw;
+    } else {
+      s.bot1[a] = bw;
     }
   }
 }
@@ -911,8 +1000,65 @@ __device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {
 //   pushboxes at x = -2 / +2 neither overlap nor touch the stage edges).
 //   Fight: frameCount = -1, recording index 0, state(-1) emitted, and the bot's
 //   first RequestNextInput.
-template <int FM, bool BOT>
-__device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
+// The handle's actors, for kActors (StepParams / ResetParams).
+struct Actors {
+  bool p1_bot;     // FS_P1_BOT
+  bool p2_resets;  // P2's bot is Reset at Intro (a bot-created P2)
+  bool p2_noop;    // a non-bot P2 presses nothing
+};
+
+// The actor input this lane's fighter gets this frame when no new action arrives (Intro, and
+// every frame for a bot): TrainingActor.GetInput() of the player's current actor.
+template <int V>
+__device__ __forceinline__ uint32_t stored_input(const Lane& L, const Actors& ac) {
+  if constexpr (V == FS_P2_BOT) return L.k == 1 ? L.bin : L.act;
+  else if constexpr (V == kActors)
+    return (L.k == 0 ? ac.p1_bot : L.p2bot) ? L.bin : ((L.k == 1 && ac.p2_noop) ? 0u : L.act);
+  else if constexpr (V == FS_P2_NOOP) return L.k == 1 ? 0u : L.act;  // an idle P2 presses nothing
+  else return L.act;
+}
+
+// TrainingManager.Step's RequestNextInput for kActors: P1's bot, then P2's (TrainingManager.cs:
+// 59-77), each on its own lane, the RNG handed from one to the other.  Both lanes must call it.
+__device__ __forceinline__ uint4 xpair4(uint4 v) {
+  uint4 o;
+  o.x = xpair(v.x);
+  o.y = xpair(v.y);
+  o.z = xpair(v.z);
+  o.w = xpair(v.w);
+  return o;
+}
+__device__ __forceinline__ void actors_request(Lane& L, const Actors& ac, float dist, uint32_t p1_act,
+                                               uint32_t p2_act) {
+  uint4 r = L.rng;
+  if (ac.p1_bot) {
+    if (L.k == 0) L.bin = bot_full_next(L.fb, r, 0, dist, p2_act);
+    const uint4 o = xpair4(r);
+    r = L.k == 1 ? o : r;
+  }
+  if (L.p2bot) {
+    if (L.k == 1) L.bin = bot_full_next(L.fb, r, 1, dist, p1_act);
+    const uint4 o = xpair4(r);
+    r = L.k == 0 ? o : r;
+  }
+  L.rng = r;
+}
+
+// The reset burst of one lane (BC:212-345).  after_ko: the KO -> End -> Stop ->
+// Intro -> Fight sequence after a terminal frame (ClearInput already applied);
+// otherwise the RESET / game-start path Stop -> Intro -> Fight.
+//   Intro: SetupBattleStart, then the bots' Reset -- P2's only when it is the bot the game was
+//   launched with (--p2-bot); a bot switched in by P2_BOT is never Reset (BC:276-277 throws on the
+//   null GameManager.botP2 first) and P1's spectator-wrapped bot is not a TrainingBattleAIActor.
+//   Intro tick: the stale actor input enters the cleared history, the frame
+//   advances unless in hitstun, RequestAction(STAND) on STAND is a no-op, and
+//   movement / boxes / pushes are no-ops (STAND has no movement window; base
+//   pushboxes at x = -2 / +2 neither overlap nor touch the stage edges).
+//   Fight: frameCount = -1, recording index 0, state(-1) emitted, and the bots'
+//   first RequestNextInput.
+template <int FM, int V>
+__device__ __forceinline__ void reset_burst(Lane& L, bool after_ko, const Actors& ac) {
+  constexpr bool BOT = V == FS_P2_BOT;
   if (after_ko) {
     const int o_vital = xpair(L.f.vital);
     end_tick(L.f, L.f.won || (L.f.vital > 0 && o_vital <= 0));  // a sole survivor wins (BC:310-323)
@@ -922,26 +1068,32 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko) {
   const uint32_t o_act = xpair((uint32_t)L.f.act);
   const float x1 = L.k == 0 ? L.f.x : o_x, x2 = L.k == 0 ? o_x : L.f.x;
   const uint32_t p1_act = L.k == 0 ? (uint32_t)L.f.act : o_act;
+  const uint32_t p2_act = L.k == 1 ? (uint32_t)L.f.act : o_act;
   if constexpr (BOT) {  // BattleAI.Reset (AI:393-403)
     L.bot.plan = L.bot.idx = 0;
     L.bot.prev_dist = bot_distance<FM>(x1, x2);
     L.bot.prev_opp = p1_act;
+  } else if constexpr (V == kActors) {
+    if (L.k == 1 && L.p2bot && ac.p2_resets) bot_full_reset(L.fb, bot_distance<FM>(x1, x2), p1_act);
   }
+  const uint32_t in = stored_input<V>(L, ac);
   if (L.rec_count < kMaxRecording) {  // RecordInput in the Intro tick (BC:333)
-    L.rec = L.act;
+    L.rec = in;
     L.rec_count++;
   }
-  const uint32_t r = rel_bits(L.act, (int)L.k);
+  const uint32_t r = rel_bits(in, (int)L.k);
   L.f.hist = (r & 1) | ((r & 2) << 15);
-  L.f.hold = (L.act & IN_ATTACK) ? 1 : 0;
+  L.f.hold = (in & IN_ATTACK) ? 1 : 0;
   const bool stunned = L.f.stun > 0;
   L.f.stun -= stunned ? 1 : 0;
   L.f.frame = stunned ? 0 : 1;
   L.frame_count = -1;
   L.rec_count = 0;
   if constexpr (BOT) {
-    const uint32_t in = bot_next_input(L.bot, L.k, bot_distance<FM>(x1, x2), p1_act);
-    L.act = L.k == 1 ? in : L.act;
+    const uint32_t bi = bot_next_input(L.bot, L.k, bot_distance<FM>(x1, x2), p1_act);
+    L.bin = L.k == 1 ? bi : L.bin;
+  } else if constexpr (V == kActors) {
+    actors_request(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
   }
 }
 
@@ -1007,8 +1159,9 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   constexpr bool BOT = P2 == FS_P2_BOT;
   const DevOutputs& o = p.out;
   const uint32_t k = L.k;
+  const Actors ac{p.p1_bot != 0, p.p2_resets != 0, p.p2_noop != 0};
   if (L.pending) {  // FS_AUTORESET_NEXT_STEP: this step runs the reset burst only
-    reset_burst<FM, BOT>(L, true);
+    reset_burst<FM, P2>(L, true, ac);
     L.pending = false;
     L.has_term = false;
     L.cum = 0.0;
@@ -1020,16 +1173,25 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     st_off(o.truncated, r, (uint8_t)0);
     return;
   }
-  // the actor inputs of this frame (TrainingManager.p1Input/p2Input, BC:383-447)
-  if (k == 0 || P2 == FS_P2_EXTERNAL) L.act = a_own;
-  else if (P2 == FS_P2_NOOP) L.act = 0;  // FS_P2_BOT: the input the bot computed after the last frame
+  // the actor inputs of this frame (TrainingManager.p1Input/p2Input, BC:383-447): a remote
+  // actor's new action, or the input a bot computed after the last frame
+  uint32_t in;
+  if constexpr (P2 == kActors) {
+    const bool mybot = k == 0 ? ac.p1_bot : L.p2bot;
+    const bool idle = k == 1 && ac.p2_noop;
+    L.act = (!mybot && !idle) ? a_own : L.act;
+    in = mybot ? L.bin : (idle ? 0u : L.act);
+  } else {
+    if (k == 0 || P2 == FS_P2_EXTERNAL) L.act = a_own;
+    in = (BOT && k == 1) ? L.bin : ((P2 == FS_P2_NOOP && k == 1) ? 0u : L.act);
+  }
   const int guard_before = L.f.guard;  // guards of FE._current_state
   L.frame_count++;
   if (L.rec_count < kMaxRecording) {  // RecordInput (BC:593-607)
-    L.rec = L.act;
+    L.rec = in;
     L.rec_count++;
   }
-  const InputEval e = update_input(L.f, L.act, (int)k);
+  const InputEval e = update_input(L.f, in, (int)k);
   const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
   increment_action_frame(L.f, ai);
   // the record if the action continues, read alongside the request's ReqInfo reads; a
@@ -1083,7 +1245,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.f.hold = 0;
     if (p.autoreset_mode == FS_AUTORESET_SAME_STEP) {
       write_final(L, o, r);
-      reset_burst<FM, BOT>(L, true);
+      reset_burst<FM, P2>(L, true, ac);
       L.cum = 0.0;
       L.has_term = false;
     } else {
@@ -1096,8 +1258,14 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
       const uint32_t o_act = xpair((uint32_t)L.f.act);
       const float x1 = k == 0 ? L.f.x : o_x, x2 = k == 0 ? o_x : L.f.x;
       const uint32_t p1_act = k == 0 ? (uint32_t)L.f.act : o_act;
-      const uint32_t in = bot_next_input(L.bot, k, bot_distance<FM>(x1, x2), p1_act);
-      L.act = k == 1 ? in : L.act;
+      const uint32_t bi = bot_next_input(L.bot, k, bot_distance<FM>(x1, x2), p1_act);
+      L.bin = k == 1 ? bi : L.bin;
+    } else if constexpr (P2 == kActors) {  // the same, for the per-arena actors
+      const float o_x = xpair(L.f.x);
+      const uint32_t o_act = xpair((uint32_t)L.f.act);
+      const float x1 = k == 0 ? L.f.x : o_x, x2 = k == 0 ? o_x : L.f.x;
+      const uint32_t p1_act = k == 0 ? (uint32_t)L.f.act : o_act, p2_act = k == 1 ? (uint32_t)L.f.act : o_act;
+      actors_request(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
     }
     L.has_term = false;
   }
@@ -1128,7 +1296,6 @@ __device__ __forceinline__ void policy_features(const Lane& L, uint32_t& d0, uin
 template <int FM, int P2, bool FUSED, bool HASH, bool POL = false>
 __device__ __forceinline__ void step_body(const StepParams& p) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  constexpr bool BOT = P2 == FS_P2_BOT;
   const bool active = l < 2 * p.n_envs;
   const int a = active ? l >> 1 : 0;
   const uint32_t k = l & 1;
@@ -1136,15 +1303,19 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   // is issued before tick t's output stores, so its wait does not drain them
   // (loads and stores retire in order on one vmcnt counter).
   const uint8_t* src = k == 0 ? p.p1 : p.p2;
-  const bool reads = POL ? (k == 1 && P2 == FS_P2_EXTERNAL) : (k == 0 || P2 == FS_P2_EXTERNAL);
+  // which lanes read an action row: P1's unless the actor or a P1 bot plays it; P2's when the handle
+  // has a remote P2 (kActors: per arena, so the row is read and ignored while the bot plays).  A
+  // handle whose P2 is the bot or idle has no P2 rows at all (p.p2 is null).
+  const bool p2_rows = P2 == FS_P2_EXTERNAL || (P2 == kActors && !p.p2_noop && !p.p2_resets);
+  const bool reads = k == 0 ? (!POL && !(P2 == kActors && p.p1_bot)) : p2_rows;
   auto fetch = [&](int t) -> uint32_t {
     if (!reads) return 0u;
-    if constexpr (HASH) return hash_action(p.action_seed, a, p.t0 + (uint64_t)t, k);
+    if constexpr (HASH) return hash_action(p.action_seed, p.arena_base + (uint64_t)a, p.t0 + (uint64_t)t, k);
     else return src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a];
   };
   // the arena state and the first action are in flight while the block stages the tables
   Lane L;
-  load_lane<BOT>(L, p.st, a, k);
+  load_lane<P2>(L, p.st, a, k);
   uint32_t next = fetch(0);
   if constexpr (POL) stage_policy(p.pol);
   stage_tables();
@@ -1165,7 +1336,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     for (int t = 0; t < p.n_steps; t++) {
       const uint32_t act = next;
       next = fetch(min(t + 1, p.n_steps - 1));
-      const PolicyOut po = policy_act(d0, d1, p.pol.seed, arena0, p.t0 + (uint64_t)t);
+      const PolicyOut po = policy_act(d0, d1, p.pol.seed, p.arena_base + arena0, p.t0 + (uint64_t)t);
       if (active) {
         const uint32_t row = (uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a;
         if (k == 0) {
@@ -1187,7 +1358,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     uint32_t none = 0;
     env_step<FM, P2>(L, next & 7u, p, (uint32_t)a, none);
   }
-  if (active) store_lane<BOT>(L, p.st, a);
+  if (active) store_lane<P2>(L, p.st, a);
 }
 
 template <int FM, int P2>
@@ -1210,8 +1381,9 @@ __global__ __launch_bounds__(256) void k_step_n_policy(StepParams p) {
   step_body<FM, P2, true, false, true>(p);
 }
 
-// FootsiesEnv.reset (FE:482-515) / RESET (BC:143-146) / game start (BC:105-128)
-template <int FM, int P2>
+// FootsiesEnv.reset (FE:482-515) / RESET (BC:143-146) / game start (BC:105-128), every handle
+// kind through the per-arena actor logic (off the throughput path).
+template <int FM>
 __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   stage_tables();
@@ -1219,9 +1391,9 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
   const int a = l >> 1;
   const uint32_t k = l & 1;
   if (!p.init && p.mask && !p.mask[a]) return;
-  constexpr bool BOT = P2 == FS_P2_BOT;
+  const Actors ac{p.p1_bot != 0, p.p2_mode == FS_P2_BOT, p.p2_mode == FS_P2_NOOP};
   Lane L;
-  if (p.init) {  // `new Fighter()` defaults (F:73-112), round state Stop
+  if (p.init) {  // `new Fighter()` defaults (F:73-112), `new BattleAI()`, round state Stop
     L.k = k;
     L.f.x = 0.0f;
     L.f.hist = 0;
@@ -1230,27 +1402,29 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
     L.f.buf = L.f.rsv = NONE;
     L.f.in_back = L.f.prox = L.f.won = false;
     L.frame_count = 0;
-    L.rec_count = L.rec = L.act = 0;
+    L.rec_count = L.rec = L.act = L.bin = 0;
     L.pending = false;
     L.has_term = true;
     L.cum = 0.0;
-    L.bot.rng = rng_init((int32_t)(uint32_t)(p.base_seed + (uint64_t)a));
-    L.bot.plan = L.bot.idx = L.bot.prev_opp = 0;
-    L.bot.prev_dist = 0.0f;
+    L.p2bot = p.p2_mode == FS_P2_BOT;
+    L.rng = rng_init((int32_t)(uint32_t)(p.base_seed + p.arena_base + (uint64_t)a));
+    L.fb.mplan = L.fb.midx = L.fb.aplan = L.fb.aidx = L.fb.prev_opp = 0;
+    L.fb.prev_dist = 0.0f;
+    L.fb.ready = false;
   } else {
-    load_lane<BOT>(L, p.st, a, k);
+    load_lane<kActors>(L, p.st, a, k);
   }
-  if (p.seeds) L.bot.rng = rng_init((int32_t)(uint32_t)p.seeds[a]);  // SEED (BC:170-173)
+  if (p.seeds) L.rng = rng_init((int32_t)(uint32_t)p.seeds[a]);  // SEED (BC:170-173)
   if (p.flags == FS_RESET_SEED_ONLY) {
-    store_lane<BOT>(L, p.st, a);
+    store_lane<kActors>(L, p.st, a);
     return;
   }
   const bool hard = p.init || p.flags == FS_RESET_HARD || !L.has_term;
   if (L.pending) {  // finish the burst Unity ran after the terminal frame
-    reset_burst<FM, BOT>(L, true);
+    reset_burst<FM, kActors>(L, true, ac);
     L.pending = false;
   }
-  if (hard) reset_burst<FM, BOT>(L, false);
+  if (hard) reset_burst<FM, kActors>(L, false, ac);
   L.cum = 0.0;
   L.has_term = p.init ? true : false;
   write_main(L, p.out, a);
@@ -1259,26 +1433,56 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
     p.out.terminated[a] = 0;
     p.out.truncated[a] = 0;
   }
-  store_lane<BOT>(L, p.st, a);
+  store_lane<kActors>(L, p.st, a);
+}
+
+// P2_BOT (BC:158-167): P2's actor of the masked arenas becomes the bot (bot = 1) or the remote actor
+__global__ __launch_bounds__(256) void k_set_p2(DevState st, int bot, const uint8_t* mask, int n) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n || (mask && !mask[a])) return;
+  const uint32_t h = (uint32_t)st.aw[a].y;
+  st.aw[a].y = (int)((h & ~(1u << 29)) | ((uint32_t)(bot != 0) << 29));
 }
 
 // synthetic action stream (fs_hash_actions), one thread per (step, arena)
 __global__ __launch_bounds__(256) void k_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0,
-                                                       uint8_t* p1, uint8_t* p2) {
+                                                       uint64_t arena_base, uint8_t* p1, uint8_t* p2) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (size_t)n_envs * n_steps) return;
-  const uint64_t env = idx % (size_t)n_envs, k = idx / (size_t)n_envs;
+  const uint64_t env = arena_base + idx % (size_t)n_envs, k = idx / (size_t)n_envs;
   p1[idx] = (uint8_t)hash_action(seed, env, t0 + k, 0);
   if (p2) p2[idx] = (uint8_t)hash_action(seed, env, t0 + k, 1);
 }
 
+// a bot word <-> its canonical fields (fs_arena_state): queues as (plan id, dequeued count),
+// plan -1 = empty; the FightState as (distance, raw opponent actionID)
+struct BotFields {
+  int32_t move_plan, move_index, attack_plan, attack_index;
+  float prev_distance;
+  int32_t prev_opponent_action;
+  uint8_t ready, input;
+};
+__device__ __forceinline__ BotFields bot_export(uint2 w) {
+  uint32_t input;
+  const FullBot b = unpack_bot(w, input);
+  BotFields f;
+  f.move_plan = b.mplan ? (int32_t)b.mplan - 1 : -1;
+  f.move_index = b.mplan ? (int32_t)b.midx : 0;
+  f.attack_plan = b.aplan ? (int32_t)b.aplan - 1 : -1;
+  f.attack_index = b.aplan ? (int32_t)b.aidx : 0;
+  f.prev_distance = b.ready ? b.prev_dist : 0.0f;  // no FightState yet: canonical zeros
+  f.prev_opponent_action = b.ready ? kActionId[b.prev_opp] : 0;
+  f.ready = b.ready;
+  f.input = (uint8_t)input;
+  return f;
+}
+
 // canonical export (fs_get_state / fs_get_env_state)
-template <bool BOT>
 __global__ __launch_bounds__(256) void k_get_state(DevState st, fs_arena_state* dst, fs_env_state* env, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Arena A;
-  load_arena<BOT>(A, st, i);
+  load_arena(A, st, i);
   if (dst) {
     fs_arena_state s;
     for (int k = 0; k < 2; k++) {
@@ -1310,24 +1514,29 @@ __global__ __launch_bounds__(256) void k_get_state(DevState st, fs_arena_state* 
     s.has_terminated = A.has_term;
     s.pad0[0] = s.pad0[1] = 0;
     s.cumulative_reward = A.cum;
-    if constexpr (BOT) {
-      s.rng[0] = A.rng.x;
-      s.rng[1] = A.rng.y;
-      s.rng[2] = A.rng.z;
-      s.rng[3] = A.rng.w;
-      s.move_plan = A.mplan ? (int32_t)A.mplan - 1 : -1;
-      s.move_index = A.mplan ? (int32_t)A.midx : 0;
-      s.attack_plan = A.aplan ? (int32_t)A.aplan - 1 : -1;
-      s.attack_index = A.aplan ? (int32_t)A.aidx : 0;
-      s.prev_distance = A.prev_dist;
-      s.prev_opponent_action = kActionId[A.prev_opp];
-    } else {
-      s.rng[0] = s.rng[1] = s.rng[2] = s.rng[3] = 0;
-      s.move_plan = s.attack_plan = -1;
-      s.move_index = s.attack_index = 0;
-      s.prev_distance = 0.0f;
-      s.prev_opponent_action = 0;
-    }
+    s.rng[0] = A.rng.x;
+    s.rng[1] = A.rng.y;
+    s.rng[2] = A.rng.z;
+    s.rng[3] = A.rng.w;
+    const BotFields b2 = bot_export(A.bw[1]), b1 = bot_export(A.bw[0]);
+    s.move_plan = b2.move_plan;
+    s.move_index = b2.move_index;
+    s.attack_plan = b2.attack_plan;
+    s.attack_index = b2.attack_index;
+    s.prev_distance = b2.prev_distance;
+    s.prev_opponent_action = b2.prev_opponent_action;
+    s.p2_bot = A.p2bot;
+    s.bot_ready[0] = b1.ready;
+    s.bot_ready[1] = b2.ready;
+    s.bot_input[0] = b1.input;
+    s.bot_input[1] = b2.input;
+    s.pad1[0] = s.pad1[1] = s.pad1[2] = 0;
+    s.p1_move_plan = b1.move_plan;
+    s.p1_move_index = b1.move_index;
+    s.p1_attack_plan = b1.attack_plan;
+    s.p1_attack_index = b1.attack_index;
+    s.p1_prev_distance = b1.prev_distance;
+    s.p1_prev_opponent_action = b1.prev_opponent_action;
     dst[i] = s;
   }
   if (env) {
@@ -1357,7 +1566,19 @@ __device__ __forceinline__ int action_index_of(int32_t id) {
   return -1;
 }
 
-template <bool BOT>
+__device__ __forceinline__ uint2 bot_import(int32_t mp, int32_t mi, int32_t ap, int32_t ai, float pd, int32_t po,
+                                           uint8_t ready, uint8_t input) {
+  FullBot b;
+  b.mplan = mp < 0 ? 0u : (uint32_t)mp + 1;
+  b.midx = mp < 0 ? 0u : (uint32_t)mi;
+  b.aplan = ap < 0 ? 0u : (uint32_t)ap + 1;
+  b.aidx = ap < 0 ? 0u : (uint32_t)ai;
+  b.prev_dist = pd;
+  b.prev_opp = (uint32_t)action_index_of(po);
+  b.ready = ready != 0;
+  return pack_bot(b, input & 7u);
+}
+
 __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_state* src, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1390,16 +1611,13 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
   A.pending = s.reset_pending;
   A.has_term = s.has_terminated;
   A.cum = s.cumulative_reward;
-  if constexpr (BOT) {
-    A.rng = make_uint4(s.rng[0], s.rng[1], s.rng[2], s.rng[3]);
-    A.mplan = s.move_plan < 0 ? 0u : (uint32_t)s.move_plan + 1;
-    A.midx = s.move_plan < 0 ? 0u : (uint32_t)s.move_index;
-    A.aplan = s.attack_plan < 0 ? 0u : (uint32_t)s.attack_plan + 1;
-    A.aidx = s.attack_plan < 0 ? 0u : (uint32_t)s.attack_index;
-    A.prev_dist = s.prev_distance;
-    A.prev_opp = (uint32_t)action_index_of(s.prev_opponent_action);
-  }
-  store_arena<BOT>(A, st, i);
+  A.rng = make_uint4(s.rng[0], s.rng[1], s.rng[2], s.rng[3]);
+  A.p2bot = s.p2_bot != 0;
+  A.bw[1] = bot_import(s.move_plan, s.move_index, s.attack_plan, s.attack_index, s.prev_distance,
+                       s.prev_opponent_action, s.bot_ready[1], s.bot_input[1]);
+  A.bw[0] = bot_import(s.p1_move_plan, s.p1_move_index, s.p1_attack_plan, s.p1_attack_index, s.p1_prev_distance,
+                       s.p1_prev_opponent_action, s.bot_ready[0], s.bot_input[0]);
+  store_arena(A, st, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -1417,53 +1635,49 @@ static void launch_step_p2(const StepParams& p, hipStream_t s) {
 }
 
 template <int FM>
-static hipError_t launch_step_fm(const StepParams& p, int p2_mode, hipStream_t s) {
-  switch (p2_mode) {
+static hipError_t launch_step_fm(const StepParams& p, int variant, hipStream_t s) {
+  switch (variant) {
     case FS_P2_EXTERNAL: launch_step_p2<FM, FS_P2_EXTERNAL>(p, s); break;
     case FS_P2_BOT: launch_step_p2<FM, FS_P2_BOT>(p, s); break;
+    case kActors: launch_step_p2<FM, kActors>(p, s); break;
     default: launch_step_p2<FM, FS_P2_NOOP>(p, s); break;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_step(const StepParams& p, int float_mode, int p2_mode, hipStream_t s) {
-  return float_mode == FS_FLOAT_DOUBLE ? launch_step_fm<FS_FLOAT_DOUBLE>(p, p2_mode, s)
-                                       : launch_step_fm<FS_FLOAT_STRICT32>(p, p2_mode, s);
+hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStream_t s) {
+  return float_mode == FS_FLOAT_DOUBLE ? launch_step_fm<FS_FLOAT_DOUBLE>(p, variant, s)
+                                       : launch_step_fm<FS_FLOAT_STRICT32>(p, variant, s);
 }
 
-template <int FM>
-static hipError_t launch_reset_fm(const ResetParams& p, int p2_mode, hipStream_t s) {
-  switch (p2_mode) {
-    case FS_P2_EXTERNAL: hipLaunchKernelGGL((k_reset<FM, FS_P2_EXTERNAL>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
-    case FS_P2_BOT: hipLaunchKernelGGL((k_reset<FM, FS_P2_BOT>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
-    default: hipLaunchKernelGGL((k_reset<FM, FS_P2_NOOP>), grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p); break;
-  }
+hipError_t launch_reset(const ResetParams& p, int float_mode, hipStream_t s) {
+  if (float_mode == FS_FLOAT_DOUBLE)
+    hipLaunchKernelGGL(k_reset<FS_FLOAT_DOUBLE>, grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p);
+  else
+    hipLaunchKernelGGL(k_reset<FS_FLOAT_STRICT32>, grid_for(2 * p.n_envs), dim3(kBlock), 0, s, p);
   return hipGetLastError();
 }
 
-hipError_t launch_reset(const ResetParams& p, int float_mode, int p2_mode, hipStream_t s) {
-  return float_mode == FS_FLOAT_DOUBLE ? launch_reset_fm<FS_FLOAT_DOUBLE>(p, p2_mode, s)
-                                       : launch_reset_fm<FS_FLOAT_STRICT32>(p, p2_mode, s);
+hipError_t launch_set_p2(const DevState& st, int bot, const uint8_t* mask, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_p2, grid_for(n), dim3(kBlock), 0, s, st, bot, mask, n);
+  return hipGetLastError();
 }
 
-hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1, uint8_t* p2,
-                               hipStream_t s) {
+hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint64_t arena_base, uint8_t* p1,
+                               uint8_t* p2, hipStream_t s) {
   const size_t total = (size_t)n_envs * n_steps;
   hipLaunchKernelGGL(k_hash_actions, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n_envs,
-                     n_steps, seed, t0, p1, p2);
+                     n_steps, seed, t0, arena_base, p1, p2);
   return hipGetLastError();
 }
 
-hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_state* env, int n, int p2_mode,
-                            hipStream_t s) {
-  if (p2_mode == FS_P2_BOT) hipLaunchKernelGGL(k_get_state<true>, grid_for(n), dim3(kBlock), 0, s, st, dst, env, n);
-  else hipLaunchKernelGGL(k_get_state<false>, grid_for(n), dim3(kBlock), 0, s, st, dst, env, n);
+hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_state* env, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_get_state, grid_for(n), dim3(kBlock), 0, s, st, dst, env, n);
   return hipGetLastError();
 }
 
-hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, int p2_mode, hipStream_t s) {
-  if (p2_mode == FS_P2_BOT) hipLaunchKernelGGL(k_set_state<true>, grid_for(n), dim3(kBlock), 0, s, st, src, n);
-  else hipLaunchKernelGGL(k_set_state<false>, grid_for(n), dim3(kBlock), 0, s, st, src, n);
+hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_state, grid_for(n), dim3(kBlock), 0, s, st, src, n);
   return hipGetLastError();
 }
 

@@ -134,7 +134,7 @@ struct PolicyOut {
 // wave's pair layout (lane 2a + k = fighter k of local arena a): `d0`, `d1` are this lane's
 // fighter features packed as bf16x2 (guard/3 | move/16, move_frame/55 | position/4.6).
 // Returns, on every lane, the action and log-probability of its own arena (l >> 1).
-__device__ __forceinline__ PolicyOut policy_act(uint32_t d0, uint32_t d1, uint64_t seed, uint32_t arena0,
+__device__ __forceinline__ PolicyOut policy_act(uint32_t d0, uint32_t d1, uint64_t seed, uint64_t arena0,
                                                 uint64_t t) {
   const int l = threadIdx.x & 63, r = l & 31, h = l >> 5;
   // gather: MFMA lane r takes arena r's two fighters (pair lanes 2r, 2r + 1)
@@ -185,7 +185,7 @@ __device__ __forceinline__ PolicyOut policy_act(uint32_t d0, uint32_t d1, uint64
   const float s_other = lane_read(s_mine, l ^ 32);
   const float s_lo = h == 0 ? s_mine : s_other, s_hi = h == 0 ? s_other : s_mine;
   const float total = s_lo + s_hi;
-  const float target = policy_uniform(seed, arena0 + (uint32_t)r, t) * total;
+  const float target = policy_uniform(seed, arena0 + (uint64_t)r, t) * total;
   // first action whose cumulative weight exceeds the target (half h = 0 starts at 0, h = 1 at s_lo)
   const float base = h == 0 ? 0.0f : s_lo;
   const float c0 = base + e0, c1 = c0 + e1, c2 = c1 + e2;

@@ -62,23 +62,21 @@ class SimBackend:
 
     def __init__(self, p2_bot=True, dense_reward=True, device=0, seed=0):
         from .simulator import FootsiesSim
-        self._kw = dict(device=device, dense_reward=dense_reward, autoreset_mode="next_step")
-        self.sim = FootsiesSim(1, p2_mode="bot" if p2_bot else "external", seed=seed, **self._kw)
-        self._bot_fields = None
-        self._seed = seed  # UnityEngine.Random's last InitState: creation seed or SEED command
+        self.sim = FootsiesSim(1, p2_mode="bot" if p2_bot else "external", seed=seed, device=device,
+                               dense_reward=dense_reward, autoreset_mode="next_step")
 
     def env_state(self):
         return self.sim.env_state()[0]
 
     def step(self, p1, p2):
-        self.sim.step(np.array([p1], np.uint8), None if p2 is None else np.array([p2], np.uint8))
+        self.sim.step(np.array([p1], np.uint8), np.array([0 if p2 is None else p2], np.uint8)
+                      if self.sim.p2_mode == "external" else None)
         return bool(self.sim.outputs_numpy()["terminated"][0])
 
     def reset(self, hard):
         self.sim.reset(hard=hard)
 
     def seed(self, seed):
-        self._seed = seed
         self.sim.reset(seeds=[np.uint64(seed & (2**64 - 1))], seed_only=True)
 
     def get_state(self):
@@ -88,27 +86,9 @@ class SimBackend:
         self.sim.set_state(st)
 
     def set_p2_bot(self, bot):
-        """Swap TrainingManager.actorP2 (BattleCore.cs:158-167): same battle, other P2 source.
-        The bot's RNG and queues persist while a remote actor plays, as the BattleAI object does."""
-        from .simulator import FootsiesSim
-        if bot == (self.sim.p2_mode == "bot"):
-            return
-        st = self.sim.get_state()
-        bot_keys = ("rng", "move_plan", "move_index", "attack_plan", "attack_index", "prev_distance",
-                    "prev_opponent_action")
-        if not bot:
-            self._bot_fields = {k: st[k].copy() for k in bot_keys}
-        old = self.sim
-        self.sim = FootsiesSim(1, p2_mode="bot" if bot else "external", **self._kw)
-        if bot and self._bot_fields is not None:
-            for k, v in self._bot_fields.items():
-                st[k] = v
-        self.sim.set_state(st)
-        if bot and self._bot_fields is None:  # the bot's first turn: the RNG as last seeded
-            st["move_plan"] = st["attack_plan"] = -1
-            self.sim.set_state(st)
-            self.sim.reset(seeds=[np.uint64(self._seed & (2**64 - 1))], seed_only=True)
-        old.close()
+        """P2_BOT (BattleCore.cs:158-167): TrainingManager.actorP2 becomes the game's P2 bot or the
+        remote actor again (fs_set_p2_mode); each keeps its own state while the other plays."""
+        self.sim.set_p2_mode("bot" if bot else "external")
 
     def close(self):
         self.sim.close()
@@ -208,8 +188,12 @@ class FootsiesServer:
             st = self.backend.get_state()
             self.backend.set_state(battle_state.load_into(st, 0, value))
         elif cmd == CMD_P2_BOT:
-            self.p2_bot = str(value).lower() == "true"
-            self.backend.set_p2_bot(self.p2_bot)
+            # TrainingRemoteControl.ProcessCommand (cs:100-102): value.ToLower() == "true".  Only a
+            # game launched with a remote P2 is served: the reference client sends P2_BOT only then
+            # (FE:468-470 raises before sending otherwise).
+            if self.p2_remote:
+                self.p2_bot = str(value).lower() == "true"
+                self.backend.set_p2_bot(self.p2_bot)
         elif cmd == CMD_SEED:
             self.backend.seed(int(value))
 

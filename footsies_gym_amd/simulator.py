@@ -13,6 +13,7 @@ from . import _abi
 from ._lib import check, lib
 
 P2_MODES = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT, "noop": _abi.FS_P2_NOOP}
+P1_MODES = {"external": _abi.FS_P1_EXTERNAL, "bot": _abi.FS_P1_BOT}
 FLOAT_MODES = {"strict": _abi.FS_FLOAT_STRICT32, "double": _abi.FS_FLOAT_DOUBLE}
 AUTORESET_MODES = {"same_step": _abi.FS_AUTORESET_SAME_STEP, "next_step": _abi.FS_AUTORESET_NEXT_STEP}
 
@@ -57,7 +58,7 @@ class FootsiesSim:
     """
 
     def __init__(self, num_envs, device=0, p2_mode="bot", dense_reward=True, float_mode="strict",
-                 autoreset_mode="same_step", seed=0, frame_delay=0):
+                 autoreset_mode="same_step", seed=0, frame_delay=0, p1_mode="external", arena_base=0):
         torch = _torch()
         if not torch.cuda.is_available():
             raise RuntimeError("FootsiesSim needs a HIP device (torch.cuda.is_available() is False)")
@@ -67,14 +68,18 @@ class FootsiesSim:
             raise ValueError("float_mode must be one of %s" % list(FLOAT_MODES))
         if autoreset_mode not in AUTORESET_MODES:
             raise ValueError("autoreset_mode must be one of %s" % list(AUTORESET_MODES))
+        if p1_mode not in P1_MODES:
+            raise ValueError("p1_mode must be one of %s" % list(P1_MODES))
         self.num_envs = int(num_envs)
         self.device = torch.device("cuda", device)
         self.p2_mode = p2_mode
+        self.p1_mode = p1_mode
         self.autoreset_mode = autoreset_mode
         cfg = _abi.fs_config(num_envs=self.num_envs, device_id=device, p2_mode=P2_MODES[p2_mode],
                              dense_reward=int(bool(dense_reward)), frame_delay=int(frame_delay),
                              float_mode=FLOAT_MODES[float_mode], autoreset_mode=AUTORESET_MODES[autoreset_mode],
-                             base_seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
+                             base_seed=int(seed) & 0xFFFFFFFFFFFFFFFF, p1_mode=P1_MODES[p1_mode],
+                             arena_base=int(arena_base))
         h = C.c_void_p()
         check(lib().fs_create(C.byref(cfg), C.byref(h)), None)
         self._h = h
@@ -116,14 +121,30 @@ class FootsiesSim:
                              flags), self._h)
         return self._out
 
+    def set_p2_mode(self, mode, mask=None):
+        """P2 of the masked arenas (all by default) becomes the in-game bot (mode "bot") or the
+        remote actor again ("external"): the P2_BOT command (fs_set_p2_mode).  Only for a sim
+        created with p2_mode="external"."""
+        if mode not in ("external", "bot"):
+            raise ValueError("mode must be 'external' or 'bot'")
+        m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(self.num_envs))
+        check(lib().fs_set_p2_mode(self._h, P2_MODES[mode], None if m is None else m.ctypes.data), self._h)
+
     def step(self, p1, p2=None, active=None):
         """One env-step of every arena.  Actions: torch uint8 device tensors [N] (fast path) or
         host arrays ((N,3) bools or (N,) ints).  active: optional [N] mask -- only those arenas
-        tick (fs_step_masked); the others keep their state and outputs."""
+        tick (fs_step_masked); the others keep their state and outputs.  With p1_mode="bot"
+        (by_example) p1 is ignored and may be None."""
         torch = _torch()
         ext = self.p2_mode == "external"
         if ext and p2 is None:
             raise ValueError("p2 actions are required when p2_mode='external'")
+        if p1 is None:
+            if self.p1_mode != "bot":
+                raise ValueError("p1 actions are required unless p1_mode='bot'")
+            p1 = np.zeros(self.num_envs, np.uint8) if not any(
+                isinstance(x, torch.Tensor) and x.is_cuda for x in (p2, active)) else torch.zeros(
+                    self.num_envs, dtype=torch.uint8, device=self.device)
         on_device = any(isinstance(x, torch.Tensor) and x.is_cuda for x in (p1, p2, active))
         if on_device:  # device path: anything on the host is moved over first
             p1 = _as_u8_device(_to_device(p1, self.device), self.num_envs)

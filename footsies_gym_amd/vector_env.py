@@ -73,7 +73,10 @@ class FootsiesVectorEnv:
       * ``None`` -> the in-game scripted bot as P2 (FE:236-237, ``--p2-bot``);
       * a callable ``opponent(obs, info) -> actions`` -> P2 driven by that policy,
         called every step with the most recent batched obs/info (FE:525-527);
-      * ``"noop"`` -> P2 never presses anything.
+        ``set_opponent`` can then switch arenas between it and the bot (FE:458-480);
+      * ``"noop"`` -> P2 never presses anything;
+    ``by_example`` (FE:83-84, 118, 230-232): the in-game bot plays P1 as well and the agent only
+    observes -- ``step`` ignores its actions (FE:522-523).
     ``output="torch"`` returns device tensors (zero-copy) instead of numpy.
     """
 
@@ -84,8 +87,6 @@ class FootsiesVectorEnv:
                  output="numpy"):
         if vs_player:
             raise ValueError("vs_player needs a human at the game window; not available in the simulator")
-        if by_example:
-            raise ValueError("by_example (the bot playing P1) is not supported")
         if not 0 <= int(frame_delay) <= _abi.FS_MAX_FRAME_DELAY:
             raise ValueError("frame_delay must be in [0, %d]" % _abi.FS_MAX_FRAME_DELAY)
         if output not in ("numpy", "torch"):
@@ -98,9 +99,11 @@ class FootsiesVectorEnv:
         p2 = "bot" if opponent is None else ("noop" if isinstance(opponent, str) and opponent == "noop" else "external")
         if p2 == "external" and not callable(opponent):
             raise ValueError("opponent must be None, 'noop' or a callable(obs, info) -> actions")
+        self.by_example = bool(by_example)
         self.sim = FootsiesSim(self.num_envs, device=device, p2_mode=p2, dense_reward=dense_reward,
                                float_mode=float_mode, autoreset_mode=autoreset_mode, seed=seed,
-                               frame_delay=frame_delay)
+                               frame_delay=frame_delay, p1_mode="bot" if by_example else "external")
+        self._p2_bot = np.zeros(self.num_envs, dtype=bool)  # arenas switched to the bot (set_opponent)
         self.single_observation_space = sp.single_observation_space()
         self.single_action_space = sp.single_action_space()
         self.observation_space = sp.batch_observation_space(self.num_envs)
@@ -126,10 +129,42 @@ class FootsiesVectorEnv:
         self._last = (obs, info)
         return obs, info
 
+    def set_opponent(self, opponent, mask=None):
+        """FootsiesEnv.set_opponent (FE:458-480): P2 of every arena (or of ``mask``) becomes the
+        callable ``opponent(obs, info) -> actions``, or the in-game bot for ``None`` -- the P2_BOT
+        command, sent only when the arena's P2 changes between the two kinds.  Like the reference,
+        it needs an environment created with a custom opponent (else RuntimeError) and returns
+        None.  A bot keeps its queues, FightState and last answer while a callable plays, and is
+        never Reset after being switched in (see fs_set_p2_mode)."""
+        if self.sim.p2_mode != "external":
+            raise RuntimeError("the environment needs to be created with a custom opponent before calling this method")
+        if opponent is not None and not callable(opponent):
+            raise ValueError("opponent must be None or a callable(obs, info) -> actions")
+        sel = np.ones(self.num_envs, dtype=bool) if mask is None else np.asarray(mask, dtype=bool).reshape(-1)
+        if opponent is None:
+            change = sel & ~self._p2_bot
+            if change.any():
+                self.sim.set_p2_mode("bot", change)
+            self._p2_bot |= sel
+        else:
+            change = sel & self._p2_bot
+            if change.any():
+                self.sim.set_p2_mode("external", change)
+            self._p2_bot &= ~sel
+            self._opponent = opponent
+
+    def _p2_actions(self):
+        """P2's actions for a remote P2 (FE:525-527); arenas whose P2 is the bot ignore theirs."""
+        if self.sim.p2_mode != "external":
+            return None
+        if self._p2_bot.all() or self._opponent is None or self._last is None:
+            return np.zeros(self.num_envs, np.uint8)
+        return self._opponent(*self._last)
+
     def step(self, actions):
-        p2 = None
-        if self.sim.p2_mode == "external":
-            p2 = self._opponent(*self._last) if self._last is not None else np.zeros(self.num_envs, np.uint8)
+        p2 = self._p2_actions()
+        if self.by_example:
+            actions = None  # FE:522-523: the bot plays P1, the agent's action is not sent
         out = self.sim.step(actions, p2)
         if self.output == "torch":
             obs = {k: out[k] for k in ("guard", "move", "move_frame", "position")}
@@ -144,9 +179,9 @@ class FootsiesVectorEnv:
         FootsiesEnv instances that are stepped at different times.  The returned batch
         holds, for inactive arenas, their previous observation with reward 0 and not
         terminated (numpy output)."""
-        p2 = None
-        if self.sim.p2_mode == "external":
-            p2 = self._opponent(*self._last) if self._last is not None else np.zeros(self.num_envs, np.uint8)
+        p2 = self._p2_actions()
+        if self.by_example:
+            actions = None
         out = self.sim.step(actions, p2, active=active)
         if self.output == "torch":
             obs = {k: out[k] for k in ("guard", "move", "move_frame", "position")}
@@ -170,8 +205,10 @@ class FootsiesVectorEnv:
         return self.sim.get_state()
 
     def load_battle_state(self, state):
-        """STATE_LOAD (BC:153-156)."""
+        """STATE_LOAD (BC:153-156) of canonical states (which carry each arena's P2 actor)."""
         self.sim.set_state(state)
+        if self.sim.p2_mode == "external":
+            self._p2_bot = np.asarray(state["p2_bot"], dtype=bool).copy()
 
     def save_battle_state_json(self, arena=0):
         """STATE_SAVE of one arena in the reference's BattleState JSON (battle_state.py)."""
@@ -206,15 +243,14 @@ class FootsiesEnv:
 
     metadata = {"render_modes": "human", "render_fps": 60}
 
-    def __init__(self, frame_delay=0, dense_reward=True, opponent=None, device=0, seed=0, **_unused):
+    def __init__(self, frame_delay=0, dense_reward=True, opponent=None, device=0, seed=0, by_example=False,
+                 **_unused):
         self._opp = opponent
-        opp = None
-        if opponent is not None:
-            opp = (lambda obs, info: np.array([encode_actions([self._opp(obs, info)])[0]], np.uint8))
         # next_step auto-reset keeps FE's handshake: a terminal step() returns the terminal
         # obs and the agent's reset() then finds the game already at state(-1) (no RESET)
-        self.venv = FootsiesVectorEnv(1, device=device, opponent=opp, dense_reward=dense_reward,
-                                      frame_delay=frame_delay, seed=seed, autoreset_mode="next_step")
+        self.venv = FootsiesVectorEnv(1, device=device, opponent=self._wrap(opponent), dense_reward=dense_reward,
+                                      frame_delay=frame_delay, seed=seed, autoreset_mode="next_step",
+                                      by_example=by_example)
         self.observation_space = self.venv.single_observation_space
         self.action_space = self.venv.single_action_space
         self.reward_range = (-1, 1)
@@ -232,6 +268,20 @@ class FootsiesEnv:
              "p2_action": tuple(bool(v) for v in info["p2_action"][0]), "p1_hitstun": int(info["p1_hitstun"][0]),
              "p2_hitstun": int(info["p2_hitstun"][0]), **o}
         return o, i
+
+    def _wrap(self, opponent):
+        """A reference opponent (obs, info) -> (left, right, attack) over the single-arena dicts
+        (FE:525-527: it sees the agent's most recent observation and info)."""
+        if opponent is None:
+            return None
+        return lambda obs, info: np.array([encode_actions([opponent(self._most_recent_observation,
+                                                                    self._most_recent_info)])[0]], np.uint8)
+
+    def set_opponent(self, opponent):
+        """FE:458-480: switch P2 between the custom opponent and the in-game bot (None).  Needs an
+        environment created with a custom opponent (RuntimeError otherwise); returns None."""
+        self.venv.set_opponent(self._wrap(opponent))
+        self._opp = opponent
 
     def reset(self, *, seed=None, options=None):
         obs, info = self.venv.reset(seed=seed, options=options)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 1
+#define FS_ABI_VERSION 2
 
 /* error codes */
 #define FS_OK 0
@@ -42,6 +42,13 @@ extern "C" {
 #define FS_P2_EXTERNAL 0  /* P2 action supplied every step (FE `opponent` callable / remote actor) */
 #define FS_P2_BOT 1       /* the in-game scripted BattleAI (BattleAI.cs:10-403) as TrainingBattleAIActor */
 #define FS_P2_NOOP 2      /* P2 input always 0 */
+
+/* P1 controller (GameManager.cs:185-200; FE:118, 230-232 `by_example`) */
+#define FS_P1_EXTERNAL 0  /* P1 action supplied every step (the agent, TrainingRemoteActor) */
+#define FS_P1_BOT 1       /* by_example: the in-game BattleAI plays P1 (--p1-bot --p1-spectator); the
+                             agent only observes.  Both bots draw from the game's one UnityEngine.Random,
+                             P1 first (TrainingManager.cs:59-77).  The spectator wrapper is not a
+                             TrainingBattleAIActor, so P1's BattleAI is never Reset (BC:274-275) */
 
 /* Float evaluation model of the C# arithmetic (parity-unpinned: no Unity binary here) */
 #define FS_FLOAT_STRICT32 0  /* every float expression rounded to IEEE binary32 per operation (default) */
@@ -77,9 +84,14 @@ typedef struct fs_config {
                               0 .. FS_MAX_FRAME_DELAY */
   int32_t float_mode;      /* FS_FLOAT_* */
   int32_t autoreset_mode;  /* FS_AUTORESET_* */
-  int32_t reserved0;
-  uint64_t base_seed;      /* arena i's bot RNG is seeded with (int32)(base_seed + i) at creation
-                              (Random.InitState, BC:170-173) */
+  int32_t p1_mode;         /* FS_P1_* */
+  uint64_t base_seed;      /* arena i's game RNG is seeded with (int32)(base_seed + arena_base + i) at
+                              creation (Random.InitState, BC:170-173) */
+  uint64_t arena_base;     /* global index of arena 0 when the arenas of one run are sharded over
+                              several handles / GPUs: the hashed action stream (fs_step_n,
+                              fs_hash_actions), the in-kernel actor's sampling stream and the creation
+                              seeds are keyed by the global index, so results do not depend on the
+                              sharding.  0 for an unsharded handle */
 } fs_config;
 
 /*
@@ -152,17 +164,33 @@ typedef struct fs_arena_state {
   int32_t frame_count;          /* BattleCore.frameCount */
   int32_t recording_count;      /* currentRecordingInputIndex, saturating at 18000 */
   uint8_t recording_last[2];    /* recordingPnInput[index-1].input */
-  uint8_t actor_input[2];       /* TrainingActor.GetInput() values (stale inputs fed to the Intro tick) */
+  uint8_t actor_input[2];       /* TrainingRemoteActor.input of the remote P1 / P2 actors: the last action
+                                   received (stale inputs fed to the Intro tick); 0 where that player has no
+                                   remote actor (a bot-created P2, FS_P2_NOOP, FS_P1_BOT) */
   uint8_t reset_pending;        /* FS_AUTORESET_NEXT_STEP: terminal, burst not yet run */
   uint8_t has_terminated;       /* FootsiesEnv.has_terminated (FE:191, 508, 563) */
   uint8_t pad0[2];
   double cumulative_reward;     /* FootsiesEnv._cummulative_episode_reward (FE:187) */
-  /* scripted bot (FS_P2_BOT) */
-  uint32_t rng[4];              /* UnityEngine.Random Xorshift128 state */
+  /* The game's UnityEngine.Random (Xorshift128 state).  One per game, shared by both bots; kept and
+     seeded in every mode, so a bot switched in later draws from the seeded stream. */
+  uint32_t rng[4];
+  /* P2's BattleAI (BattleAI.cs:26-32) */
   int32_t move_plan, move_index;     /* moveQueue as (plan id, dequeued count); plan -1 = empty */
   int32_t attack_plan, attack_index; /* attackQueue likewise */
   float prev_distance;          /* BattleAI.fightStates[5] (== previous call's state) */
   int32_t prev_opponent_action; /* raw actionID of the opponent in that FightState */
+  /* actors (ABI 2) */
+  uint8_t p2_bot;               /* 1: TrainingManager.actorP2 is the bot (FS_P2_BOT handles always; an
+                                   FS_P2_EXTERNAL handle after fs_set_p2_mode) */
+  uint8_t bot_ready[2];         /* P1 / P2 BattleAI: fightStates[5] is set, i.e. getNextAIInput has run
+                                   since construction or Reset (AI:41-47); 0 = its next call returns 0 */
+  uint8_t bot_input[2];         /* TrainingBattleAIActor.input of the P1 / P2 bot (its last answer) */
+  uint8_t pad1[3];
+  /* P1's BattleAI (FS_P1_BOT), fields as P2's */
+  int32_t p1_move_plan, p1_move_index;
+  int32_t p1_attack_plan, p1_attack_index;
+  float p1_prev_distance;
+  int32_t p1_prev_opponent_action;
 } fs_arena_state;
 
 typedef struct fs_context* fs_handle;
@@ -183,10 +211,23 @@ int fs_create(const fs_config* cfg, fs_handle* out);
  * outputs (reward 0, terminated 0). */
 int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int flags);
 
+/* Switch P2 of the masked arenas (host [N] 0/1, NULL = all) between the remote actor
+ * (FS_P2_EXTERNAL) and the in-game bot (FS_P2_BOT): the P2_BOT remote-control command
+ * (BC:158-167, TrainingRemoteControl.cs:100-102) that FootsiesEnv.set_opponent sends
+ * (FE:458-480).  Only for handles created with FS_P2_EXTERNAL -- the reference needs a
+ * custom opponent to accept the command (FE:468-470) -- else FS_E_UNSUPPORTED.  The
+ * switch applies from the next tick.  The bot keeps its own state while inactive (queues,
+ * FightState, last answer), the remote actor its last received action.  Since such a game
+ * was launched without --p2-bot, BattleCore's Intro throws before it could Reset the
+ * switched-in bot (BC:276-277, GameManager.cs:187), so that bot is never Reset. */
+int fs_set_p2_mode(fs_handle h, int mode, const uint8_t* mask);
+
 /* One Fight tick of every arena (FootsiesEnv.step, FE:518-570 -> BC:201-220,
  * 347-364), with auto-reset of terminated arenas per cfg.autoreset_mode.
- * p1_act: [N] 3-bit inputs (Left=1, Right=2, Attack=4; InputData.cs:8-14).
- * p2_act: [N] for FS_P2_EXTERNAL, ignored (may be NULL) otherwise.
+ * p1_act: [N] 3-bit inputs (Left=1, Right=2, Attack=4; InputData.cs:8-14); ignored (may be
+ * NULL) for FS_P1_BOT.
+ * p2_act: [N] for FS_P2_EXTERNAL (read for the arenas whose P2 is the remote actor),
+ * ignored (may be NULL) otherwise.
  * flags: FS_ACT_HOST or FS_ACT_DEVICE for where the action arrays live. */
 int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags);
 
@@ -200,7 +241,7 @@ int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, co
 /* n Fight ticks in one kernel launch (fused rollout).  Actions: device arrays
  * [n][N], or NULL to draw them on device from the counter-based hash
  * a = splitmix64(action_seed ^ env*0x9E3779B97F4A7C15 ^ (t << 1 | player)) & 7
- * with t = fs_steps_taken(h) + k.  traj: device arrays laid out [n][N] (pairs
+ * with env = cfg.arena_base + i and t = fs_steps_taken(h) + k.  traj: device arrays laid out [n][N] (pairs
  * [n][N][2]) receiving every tick's outputs; traj == NULL writes each tick
  * into the handle's regular outputs (the last tick remains visible; with
  * frame_delay > 0 the n ticks are then launched one by one, since the delayed
@@ -236,7 +277,7 @@ typedef struct fs_policy {
 int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint8_t* p2_act, const fs_outputs* traj);
 
 /* Fill device arrays p1_out/p2_out [n_steps][N] with the synthetic action stream
- * of fs_step_n (splitmix64 hash of (seed, env, t0 + k, player)),
+ * of fs_step_n (splitmix64 hash of (seed, arena_base + i, t0 + k, player)),
  * so benchmark inputs are resident in HBM before the timed region.
  * p2_out may be NULL. */
 int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out);

@@ -36,6 +36,7 @@ def lib():
         L.or_create.argtypes = [C.POINTER(abi.fs_config), C.POINTER(C.c_void_p)]
         L.or_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.or_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_set_p2_mode.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.or_step_masked.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_step_n_hashed.argtypes = [C.c_void_p, C.c_int, C.c_uint64]
         L.or_outputs_get.argtypes = [C.c_void_p, C.POINTER(abi.fs_outputs)]
@@ -68,11 +69,12 @@ class Oracle:
     """Host-side mirror of the fs_* API over the CPU oracle."""
 
     def __init__(self, num_envs, p2_mode=abi.FS_P2_EXTERNAL, dense_reward=True, float_mode=abi.FS_FLOAT_STRICT32,
-                 autoreset_mode=abi.FS_AUTORESET_SAME_STEP, base_seed=0, frame_delay=0):
+                 autoreset_mode=abi.FS_AUTORESET_SAME_STEP, base_seed=0, frame_delay=0, p1_mode=abi.FS_P1_EXTERNAL,
+                 arena_base=0):
         L = lib()
         cfg = abi.fs_config(num_envs=num_envs, device_id=-1, p2_mode=p2_mode, dense_reward=int(dense_reward),
                             frame_delay=frame_delay, float_mode=float_mode, autoreset_mode=autoreset_mode,
-                            base_seed=base_seed)
+                            base_seed=base_seed, p1_mode=p1_mode, arena_base=arena_base)
         h = C.c_void_p()
         rc = L.or_create(C.byref(cfg), C.byref(h))
         if rc != 0:
@@ -101,15 +103,20 @@ class Oracle:
         assert rc == 0, rc
         return self.outputs()
 
+    def set_p2_mode(self, mode, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        return lib().or_set_p2_mode(self.h, mode, None if m is None else m.ctypes.data)
+
     def step(self, p1, p2=None, active=None):
-        p1 = np.ascontiguousarray(p1, dtype=np.uint8)
+        p1 = None if p1 is None else np.ascontiguousarray(p1, dtype=np.uint8)
         p2 = None if p2 is None else np.ascontiguousarray(p2, dtype=np.uint8)
+        q1 = None if p1 is None else p1.ctypes.data
         q2 = None if p2 is None else p2.ctypes.data
         if active is None:
-            rc = lib().or_step(self.h, p1.ctypes.data, q2)
+            rc = lib().or_step(self.h, q1, q2)
         else:
             m = np.ascontiguousarray(active, dtype=np.uint8)
-            rc = lib().or_step_masked(self.h, p1.ctypes.data, q2, m.ctypes.data)
+            rc = lib().or_step_masked(self.h, q1, q2, m.ctypes.data)
         assert rc == 0, rc
         return self.outputs()
 

@@ -166,9 +166,11 @@ typedef struct {
   int frame_count;
   uint32_t rec_idx;          /* currentRecordingInputIndex (BC:70) */
   int rec_last[2];           /* recordingPnInput[rec_idx - 1].input */
-  int actor_in[2];           /* TrainingActor.GetInput() */
-  uint32_t rng[4];
-  bot_t bot;
+  int actor_in[2];           /* TrainingRemoteActor.input of the remote P1 / P2 actors */
+  int bot_in[2];             /* TrainingBattleAIActor.input of P1's / P2's bot */
+  int p2_bot;                /* TrainingManager.actorP2 is the bot (BC:158-167) */
+  uint32_t rng[4];           /* the game's one UnityEngine.Random, shared by both bots */
+  bot_t bot[2];              /* P1's BattleAI (isPlayer1, by_example) and P2's */
   /* FootsiesEnv side */
   fs_env_state cur_state;    /* FE._current_state */
   double cum_reward;         /* FE._cummulative_episode_reward */
@@ -572,31 +574,32 @@ static int q_pop(queue_t* q) {
   return v;
 }
 
-static int bot_forward(void) { return IN_LEFT; }   /* AI:380-383 with isPlayer1 = false */
-static int bot_backward(void) { return IN_RIGHT; } /* AI:385-388 */
+/* GetForwardInput / GetBackwardInput (AI:380-388): P1's bot (isPlayer1) walks Right */
+static int bot_forward(int k) { return k == 0 ? IN_RIGHT : IN_LEFT; }
+static int bot_backward(int k) { return k == 0 ? IN_LEFT : IN_RIGHT; }
 
-static void add_forward(bot_t* b, int n) { for (int i = 0; i < n; i++) q_push(&b->move_q, bot_forward()); }
-static void add_backward(bot_t* b, int n) { for (int i = 0; i < n; i++) q_push(&b->move_q, bot_backward()); }
-static void add_forward_dash(bot_t* b) { /* AI:330-335 */
-  q_push(&b->move_q, bot_forward());
+static void add_forward(bot_t* b, int k, int n) { for (int i = 0; i < n; i++) q_push(&b->move_q, bot_forward(k)); }
+static void add_backward(bot_t* b, int k, int n) { for (int i = 0; i < n; i++) q_push(&b->move_q, bot_backward(k)); }
+static void add_forward_dash(bot_t* b, int k) { /* AI:330-335 */
+  q_push(&b->move_q, bot_forward(k));
   q_push(&b->move_q, 0);
-  q_push(&b->move_q, bot_forward());
+  q_push(&b->move_q, bot_forward(k));
 }
-static void add_backward_dash(bot_t* b) { /* AI:337-342: enqueues *forward* inputs (reference quirk) */
-  q_push(&b->move_q, bot_forward());
+static void add_backward_dash(bot_t* b, int k) { /* AI:337-342: enqueues *forward* inputs (reference quirk) */
+  q_push(&b->move_q, bot_forward(k));
   q_push(&b->move_q, 0);
-  q_push(&b->move_q, bot_forward());
+  q_push(&b->move_q, bot_forward(k));
 }
 
-static void set_move_plan(bot_t* b, int plan) {
+static void set_move_plan(bot_t* b, int k, int plan) {
   switch (plan) {
     case MP_NEUTRAL: for (int i = 0; i < 30; i++) q_push(&b->move_q, 0); break;           /* AI:192-200 */
-    case MP_FAR1: add_forward(b, 40); add_backward(b, 10); add_forward(b, 30); add_backward(b, 10); break;
-    case MP_FAR2: add_forward_dash(b); add_backward(b, 25); add_forward_dash(b); add_backward(b, 25); break;
-    case MP_MID1: add_forward(b, 30); add_backward(b, 10); add_forward(b, 20); add_backward(b, 10); break;
-    case MP_MID2: add_forward_dash(b); add_backward(b, 30); break;
-    case MP_FALLBACK1: add_backward(b, 60); break;
-    case MP_FALLBACK2: add_backward_dash(b); add_backward(b, 60); break;
+    case MP_FAR1: add_forward(b, k, 40); add_backward(b, k, 10); add_forward(b, k, 30); add_backward(b, k, 10); break;
+    case MP_FAR2: add_forward_dash(b, k); add_backward(b, k, 25); add_forward_dash(b, k); add_backward(b, k, 25); break;
+    case MP_MID1: add_forward(b, k, 30); add_backward(b, k, 10); add_forward(b, k, 20); add_backward(b, k, 10); break;
+    case MP_MID2: add_forward_dash(b, k); add_backward(b, k, 30); break;
+    case MP_FALLBACK1: add_backward(b, k, 60); break;
+    case MP_FALLBACK2: add_backward_dash(b, k); add_backward(b, k, 60); break;
   }
   b->move_plan = plan;
   b->move_len = b->move_q.count;
@@ -629,40 +632,40 @@ static void set_attack_plan(bot_t* b, int plan) {
   b->attack_len = q->count;
 }
 
-static void select_movement(arena_t* A, const fight_state_t* s) { /* AI:68-126 */
-  bot_t* b = &A->bot;
+static void select_movement(arena_t* A, int k, const fight_state_t* s) { /* AI:68-126 */
+  bot_t* b = &A->bot[k];
   if (s->distance_x > 4.0f) {
     int r = rng_range(A->rng, 0, 2);
-    set_move_plan(b, r == 0 ? MP_FAR1 : MP_FAR2);
+    set_move_plan(b, k, r == 0 ? MP_FAR1 : MP_FAR2);
   } else if (s->distance_x > 3.0f) {
     int r = rng_range(A->rng, 0, 7);
-    if (r <= 1) set_move_plan(b, MP_MID1);
-    else if (r <= 3) set_move_plan(b, MP_MID2);
-    else if (r == 4) set_move_plan(b, MP_FAR1);
-    else if (r == 5) set_move_plan(b, MP_FAR2);
-    else set_move_plan(b, MP_NEUTRAL);
+    if (r <= 1) set_move_plan(b, k, MP_MID1);
+    else if (r <= 3) set_move_plan(b, k, MP_MID2);
+    else if (r == 4) set_move_plan(b, k, MP_FAR1);
+    else if (r == 5) set_move_plan(b, k, MP_FAR2);
+    else set_move_plan(b, k, MP_NEUTRAL);
   } else if (s->distance_x > 2.5f) {
     int r = rng_range(A->rng, 0, 5);
-    if (r == 0) set_move_plan(b, MP_MID1);
-    else if (r == 1) set_move_plan(b, MP_MID2);
-    else if (r == 2) set_move_plan(b, MP_FALLBACK1);
-    else if (r == 3) set_move_plan(b, MP_FALLBACK2);
-    else set_move_plan(b, MP_NEUTRAL);
+    if (r == 0) set_move_plan(b, k, MP_MID1);
+    else if (r == 1) set_move_plan(b, k, MP_MID2);
+    else if (r == 2) set_move_plan(b, k, MP_FALLBACK1);
+    else if (r == 3) set_move_plan(b, k, MP_FALLBACK2);
+    else set_move_plan(b, k, MP_NEUTRAL);
   } else if (s->distance_x > 2.0f) {
     int r = rng_range(A->rng, 0, 4);
-    if (r == 0) set_move_plan(b, MP_FALLBACK1);
-    else if (r == 1) set_move_plan(b, MP_FALLBACK2);
-    else set_move_plan(b, MP_NEUTRAL);
+    if (r == 0) set_move_plan(b, k, MP_FALLBACK1);
+    else if (r == 1) set_move_plan(b, k, MP_FALLBACK2);
+    else set_move_plan(b, k, MP_NEUTRAL);
   } else {
     int r = rng_range(A->rng, 0, 3);
-    if (r == 0) set_move_plan(b, MP_FALLBACK1);
-    else if (r == 1) set_move_plan(b, MP_FALLBACK2);
-    else set_move_plan(b, MP_NEUTRAL);
+    if (r == 0) set_move_plan(b, k, MP_FALLBACK1);
+    else if (r == 1) set_move_plan(b, k, MP_FALLBACK2);
+    else set_move_plan(b, k, MP_NEUTRAL);
   }
 }
 
-static void select_attack(arena_t* A, const fight_state_t* s) { /* AI:128-190 */
-  bot_t* b = &A->bot;
+static void select_attack(arena_t* A, int k, const fight_state_t* s) { /* AI:128-190 */
+  bot_t* b = &A->bot[k];
   if (s->opp_damage || s->opp_guard_break || s->opp_special_attack) {
     set_attack_plan(b, AP_TWO_HIT);
   } else if (s->distance_x > 4.0f) {
@@ -696,8 +699,9 @@ static void select_attack(arena_t* A, const fight_state_t* s) { /* AI:128-190 */
   }
 }
 
-static void bot_update_fight_state(arena_t* A, int fm) { /* AI:344-363 */
-  const fighter_t* opp = &A->f[0];
+/* the bot of fighter k (0 = P1, isPlayer1; 1 = P2); its opponent is the other fighter (AI:34-39) */
+static void bot_update_fight_state(arena_t* A, int k, int fm) { /* AI:344-363 */
+  const fighter_t* opp = &A->f[1 - k];
   fight_state_t cur;
   memset(&cur, 0, sizeof cur);
   cur.valid = 1;
@@ -710,28 +714,30 @@ static void bot_update_fight_state(arena_t* A, int fm) { /* AI:344-363 */
   cur.opp_special_attack = opp->action_id == N_SPECIAL || opp->action_id == B_SPECIAL;
   cur.opp_action = opp->action_id;
   /* the reference's ascending copy loop: every slot 1..9 ends up equal to the old slot 0 */
-  for (int i = 1; i < 10; i++) A->bot.fs[i] = A->bot.fs[i - 1];
-  A->bot.fs[0] = cur;
+  for (int i = 1; i < 10; i++) A->bot[k].fs[i] = A->bot[k].fs[i - 1];
+  A->bot[k].fs[0] = cur;
 }
 
-static void bot_reset(arena_t* A, int fm) { /* AI:393-403 */
-  q_clear(&A->bot.move_q);
-  q_clear(&A->bot.attack_q);
-  A->bot.move_plan = A->bot.attack_plan = -1;
-  A->bot.move_len = A->bot.attack_len = 0;
-  bot_update_fight_state(A, fm);
-  for (int i = 0; i < 10; i++) A->bot.fs[i] = A->bot.fs[0];
+static void bot_reset(arena_t* A, int k, int fm) { /* AI:393-403 */
+  bot_t* b = &A->bot[k];
+  q_clear(&b->move_q);
+  q_clear(&b->attack_q);
+  b->move_plan = b->attack_plan = -1;
+  b->move_len = b->attack_len = 0;
+  bot_update_fight_state(A, k, fm);
+  for (int i = 0; i < 10; i++) b->fs[i] = b->fs[0];
 }
 
-static int bot_get_next_input(arena_t* A, int fm) { /* AI:41-66 */
+static int bot_get_next_input(arena_t* A, int k, int fm) { /* AI:41-66 */
   int input = 0;
-  bot_update_fight_state(A, fm);
-  const fight_state_t* s = &A->bot.fs[5]; /* fightStateReadIndex (AI:32) */
+  bot_t* b = &A->bot[k];
+  bot_update_fight_state(A, k, fm);
+  const fight_state_t* s = &b->fs[5]; /* fightStateReadIndex (AI:32); null until a second call or a Reset */
   if (s->valid) {
-    if (A->bot.move_q.count > 0) input |= q_pop(&A->bot.move_q);
-    else select_movement(A, s);
-    if (A->bot.attack_q.count > 0) input |= q_pop(&A->bot.attack_q);
-    else select_attack(A, s);
+    if (b->move_q.count > 0) input |= q_pop(&b->move_q);
+    else select_movement(A, k, s);
+    if (b->attack_q.count > 0) input |= q_pop(&b->attack_q);
+    else select_attack(A, k, s);
   }
   return input;
 }
@@ -850,8 +856,16 @@ static void hitbox_hurtbox_collision(arena_t* A, int fm) { /* BC:521-591 */
   }
 }
 
-static void update_intro_state(arena_t* A, int fm) { /* BC:329-345 */
-  int p1 = A->actor_in[0], p2 = A->actor_in[1];
+/* TrainingManager.p1Input / p2Input (TrainingManager.cs:79-87): the current actor's GetInput() --
+   the bot's last answer, or the remote actor's last received action (0 for an idle P2) */
+static int get_input(const or_ctx* C, const arena_t* A, int k) {
+  if (k == 0) return C->cfg.p1_mode == FS_P1_BOT ? A->bot_in[0] : A->actor_in[0];
+  if (A->p2_bot) return A->bot_in[1];
+  return C->cfg.p2_mode == FS_P2_NOOP ? 0 : A->actor_in[1];
+}
+
+static void update_intro_state(const or_ctx* C, arena_t* A, int fm) { /* BC:329-345 */
+  int p1 = get_input(C, A, 0), p2 = get_input(C, A, 1);
   record_input(A, p1, p2);
   update_input(&A->f[0], p1);
   update_input(&A->f[1], p2);
@@ -863,8 +877,8 @@ static void update_intro_state(arena_t* A, int fm) { /* BC:329-345 */
   push_character_vs_background(A, fm);
 }
 
-static void update_fight_state(arena_t* A, int fm) { /* BC:347-364 */
-  int p1 = A->actor_in[0], p2 = A->actor_in[1];
+static void update_fight_state(const or_ctx* C, arena_t* A, int fm) { /* BC:347-364 */
+  int p1 = get_input(C, A, 0), p2 = get_input(C, A, 1);
   record_input(A, p1, p2);
   update_input(&A->f[0], p1);
   update_input(&A->f[1], p2);
@@ -886,13 +900,17 @@ static void update_end_state(arena_t* A, int fm) { /* BC:371-381 */
   push_character_vs_background(A, fm);
 }
 
-/* TrainingManager.Step (TrainingManager.cs:59-77) with P1 a remote actor and P2
- * the bot (RequestNextInput -> getNextAIInput, TrainingBattleAIActor.cs:38-41) or remote */
+/* TrainingManager.Step (TrainingManager.cs:59-77): P1's actor, then P2's, request their next
+ * input unless the battle is over.  A bot answers at once (RequestNextInput -> getNextAIInput,
+ * TrainingBattleAIActor.cs:38-41), drawing from the game's one RNG in that order; a remote actor's
+ * answer is the action the next step delivers (fe_step_arena). */
 static void training_step(or_ctx* C, arena_t* A, int battle_over) {
   A->emitted = 1;
   A->emitted_battle_over = battle_over;
   A->emitted_state = get_environment_state(A);
-  if (!battle_over && C->cfg.p2_mode == FS_P2_BOT) A->actor_in[1] = bot_get_next_input(A, C->cfg.float_mode);
+  if (battle_over) return;
+  if (C->cfg.p1_mode == FS_P1_BOT) A->bot_in[0] = bot_get_next_input(A, 0, C->cfg.float_mode);
+  if (A->p2_bot) A->bot_in[1] = bot_get_next_input(A, 1, C->cfg.float_mode);
 }
 
 static void change_round_state(or_ctx* C, arena_t* A, int state) { /* BC:247-327 */
@@ -904,7 +922,12 @@ static void change_round_state(or_ctx* C, arena_t* A, int state) { /* BC:247-327
       setup_battle_start(&A->f[0], OR_P1_START_X, 1);
       setup_battle_start(&A->f[1], OR_P2_START_X, 0);
       A->timer = 0.0f; /* introStateTime = 0 in training (BC:124-127) */
-      if (C->cfg.p2_mode == FS_P2_BOT) bot_reset(A, fm);
+      /* BC:274-277: only a TrainingBattleAIActor is Reset, through GameManager.botP1 / botP2.  P1's
+         bot is wrapped in a spectator (by_example), so it never is; P2's is when the game was
+         launched with --p2-bot.  A bot switched in by P2_BOT in a game launched with a remote P2
+         finds botP2 null: the Intro throws there, after SetupBattleStart, and nothing else of this
+         ChangeRoundState runs -- the bot keeps its queues and FightStates. */
+      if (A->p2_bot && C->cfg.p2_mode == FS_P2_BOT) bot_reset(A, 1, fm);
       break;
     case RS_FIGHT:
       A->frame_count = -1;
@@ -937,14 +960,14 @@ static void fixed_update(or_ctx* C, arena_t* A, int cmd) {
       change_round_state(C, A, RS_INTRO);
       break;
     case RS_INTRO:
-      update_intro_state(A, fm);
+      update_intro_state(C, A, fm);
       A->timer -= OR_FIXED_DT;
       if (A->timer <= 0.0f) change_round_state(C, A, RS_FIGHT);
       break;
     case RS_FIGHT: {
       /* synced mode: the driver only calls this once the actions are in (TrainingManager.Ready) */
       A->frame_count++;
-      update_fight_state(A, fm);
+      update_fight_state(C, A, fm);
       int battle_over = A->f[0].vital <= 0 || A->f[1].vital <= 0;
       if (battle_over) change_round_state(C, A, RS_KO);
       training_step(C, A, battle_over);
@@ -1074,9 +1097,8 @@ static void fe_step_arena(or_ctx* C, int i, int p1, int p2) {
     return;
   }
   /* the actions arrive; the synced game runs its Fight tick (TrainingRemoteActor.cs:93-117) */
-  A->actor_in[0] = p1 & 7;
-  if (C->cfg.p2_mode == FS_P2_EXTERNAL) A->actor_in[1] = p2 & 7;
-  else if (C->cfg.p2_mode == FS_P2_NOOP) A->actor_in[1] = 0;
+  if (C->cfg.p1_mode != FS_P1_BOT) A->actor_in[0] = p1 & 7;                  /* by_example sends none (FE:522-523) */
+  if (C->cfg.p2_mode == FS_P2_EXTERNAL && !A->p2_bot) A->actor_in[1] = p2 & 7; /* FE:525-527 */
   fs_env_state prev = A->cur_state;
   fs_env_state st = run_until_emission(C, A, 0);
   A->cur_state = st;
@@ -1131,6 +1153,7 @@ OR_EXPORT int or_create(const fs_config* cfg, or_handle* out) {
   if (!cfg || !out || cfg->num_envs <= 0) return FS_E_INVALID;
   if (cfg->frame_delay < 0) return FS_E_INVALID;
   if (cfg->p2_mode < 0 || cfg->p2_mode > 2) return FS_E_INVALID;
+  if (cfg->p1_mode != FS_P1_EXTERNAL && cfg->p1_mode != FS_P1_BOT) return FS_E_INVALID;
   or_ctx* C = (or_ctx*)xcalloc(1, sizeof(or_ctx));
   C->cfg = *cfg;
   int n = C->n = cfg->num_envs;
@@ -1158,8 +1181,9 @@ OR_EXPORT int or_create(const fs_config* cfg, or_handle* out) {
     new_fighter(&A->f[0]);
     new_fighter(&A->f[1]);
     A->round_state = RS_STOP;
-    A->bot.move_plan = A->bot.attack_plan = -1;
-    rng_init(A->rng, (int32_t)(uint32_t)(cfg->base_seed + (uint64_t)i));
+    A->bot[0].move_plan = A->bot[0].attack_plan = A->bot[1].move_plan = A->bot[1].attack_plan = -1;
+    A->p2_bot = cfg->p2_mode == FS_P2_BOT; /* GameManager.cs:193 (--p2-bot) */
+    rng_init(A->rng, (int32_t)(uint32_t)(cfg->base_seed + cfg->arena_base + (uint64_t)i));
     /* game start: Stop -> Intro -> Fight, state(-1) emitted */
     A->cur_state = run_until_emission(C, A, 0);
     A->has_terminated = 1; /* FE.__init__ (FE:191): the first reset() sends no RESET */
@@ -1187,11 +1211,20 @@ OR_EXPORT int or_reset(or_handle C, const uint64_t* seeds, const uint8_t* mask, 
   return FS_OK;
 }
 
+/* P2_BOT (BC:158-167) on the masked arenas: P2's actor becomes the bot or the remote actor again */
+OR_EXPORT int or_set_p2_mode(or_handle C, int mode, const uint8_t* mask) {
+  if (!C || (mode != FS_P2_EXTERNAL && mode != FS_P2_BOT)) return FS_E_INVALID;
+  if (C->cfg.p2_mode != FS_P2_EXTERNAL) return FS_E_UNSUPPORTED;
+  for (int i = 0; i < C->n; i++)
+    if (!mask || mask[i]) C->a[i].p2_bot = mode == FS_P2_BOT;
+  return FS_OK;
+}
+
 OR_EXPORT int or_step(or_handle C, const uint8_t* p1, const uint8_t* p2) {
-  if (!C || !p1) return FS_E_INVALID;
+  if (!C || (!p1 && C->cfg.p1_mode != FS_P1_BOT)) return FS_E_INVALID;
   if (C->cfg.p2_mode == FS_P2_EXTERNAL && !p2) return FS_E_INVALID;
 #pragma omp parallel for schedule(static) if (C->n >= 1024)
-  for (int i = 0; i < C->n; i++) fe_step_arena(C, i, p1[i], p2 ? p2[i] : 0);
+  for (int i = 0; i < C->n; i++) fe_step_arena(C, i, p1 ? p1[i] : 0, p2 ? p2[i] : 0);
   C->steps++;
   return FS_OK;
 }
@@ -1199,12 +1232,12 @@ OR_EXPORT int or_step(or_handle C, const uint8_t* p1, const uint8_t* p2) {
 /* fs_step_masked: only arenas with active[i] != 0 run FootsiesEnv.step; the others are
    separate environments that were not stepped (state and outputs untouched) */
 OR_EXPORT int or_step_masked(or_handle C, const uint8_t* p1, const uint8_t* p2, const uint8_t* active) {
-  if (!C || !p1 || !active) return FS_E_INVALID;
+  if (!C || (!p1 && C->cfg.p1_mode != FS_P1_BOT) || !active) return FS_E_INVALID;
   if (C->cfg.p2_mode == FS_P2_EXTERNAL && !p2) return FS_E_INVALID;
   if (C->cfg.frame_delay > 0) return FS_E_UNSUPPORTED;
 #pragma omp parallel for schedule(static) if (C->n >= 1024)
   for (int i = 0; i < C->n; i++)
-    if (active[i]) fe_step_arena(C, i, p1[i], p2 ? p2[i] : 0);
+    if (active[i]) fe_step_arena(C, i, p1 ? p1[i] : 0, p2 ? p2[i] : 0);
   C->steps++;
   return FS_OK;
 }
@@ -1226,9 +1259,11 @@ OR_EXPORT int or_step_n_hashed(or_handle C, int n, uint64_t action_seed) {
   uint64_t t0 = C->steps;
 #pragma omp parallel for schedule(static) if (C->n >= 1024)
   for (int i = 0; i < C->n; i++)
-    for (int k = 0; k < n; k++)
-      fe_step_arena(C, i, or_hash_action(action_seed, (uint64_t)i, t0 + (uint64_t)k, 0),
-                    or_hash_action(action_seed, (uint64_t)i, t0 + (uint64_t)k, 1));
+    for (int k = 0; k < n; k++) {
+      const uint64_t env = C->cfg.arena_base + (uint64_t)i;
+      fe_step_arena(C, i, or_hash_action(action_seed, env, t0 + (uint64_t)k, 0),
+                    or_hash_action(action_seed, env, t0 + (uint64_t)k, 1));
+    }
   C->steps += (uint64_t)n;
   return FS_OK;
 }
@@ -1259,6 +1294,19 @@ OR_EXPORT int or_get_env_state(or_handle C, fs_env_state* out) {
   if (!C || !out) return FS_E_INVALID;
   for (int i = 0; i < C->n; i++) out[i] = get_environment_state(&C->a[i]);
   return FS_OK;
+}
+
+/* a BattleAI in canonical form: queues as (plan, dequeued count), plan -1 = empty; the FightState
+   its next call reads (fightStates[5] == slot 0 after the ascending copy, AI:358-361) */
+static void bot_export(const bot_t* b, int32_t* mp, int32_t* mi, int32_t* ap, int32_t* ai, float* pd, int32_t* po,
+                       uint8_t* ready) {
+  *mp = b->move_q.count > 0 ? b->move_plan : -1;
+  *mi = b->move_q.count > 0 ? b->move_len - b->move_q.count : 0;
+  *ap = b->attack_q.count > 0 ? b->attack_plan : -1;
+  *ai = b->attack_q.count > 0 ? b->attack_len - b->attack_q.count : 0;
+  *pd = b->fs[0].valid ? b->fs[0].distance_x : 0.0f;
+  *po = b->fs[0].valid ? b->fs[0].opp_action : STAND;
+  *ready = (uint8_t)b->fs[0].valid;
 }
 
 OR_EXPORT int or_get_state(or_handle C, fs_arena_state* out) {
@@ -1298,17 +1346,14 @@ OR_EXPORT int or_get_state(or_handle C, fs_arena_state* out) {
     s->reset_pending = (uint8_t)A->reset_pending;
     s->has_terminated = (uint8_t)A->has_terminated;
     s->cumulative_reward = A->cum_reward;
-    if (C->cfg.p2_mode == FS_P2_BOT) {
-      memcpy(s->rng, A->rng, sizeof s->rng);
-      s->move_plan = A->bot.move_q.count > 0 ? A->bot.move_plan : -1;
-      s->move_index = A->bot.move_q.count > 0 ? A->bot.move_len - A->bot.move_q.count : 0;
-      s->attack_plan = A->bot.attack_q.count > 0 ? A->bot.attack_plan : -1;
-      s->attack_index = A->bot.attack_q.count > 0 ? A->bot.attack_len - A->bot.attack_q.count : 0;
-      s->prev_distance = A->bot.fs[0].distance_x; /* == fs[5] on the next call */
-      s->prev_opponent_action = A->bot.fs[0].opp_action;
-    } else {
-      s->move_plan = s->attack_plan = -1;
-    }
+    memcpy(s->rng, A->rng, sizeof s->rng);
+    bot_export(&A->bot[1], &s->move_plan, &s->move_index, &s->attack_plan, &s->attack_index, &s->prev_distance,
+               &s->prev_opponent_action, &s->bot_ready[1]);
+    bot_export(&A->bot[0], &s->p1_move_plan, &s->p1_move_index, &s->p1_attack_plan, &s->p1_attack_index,
+               &s->p1_prev_distance, &s->p1_prev_opponent_action, &s->bot_ready[0]);
+    s->p2_bot = (uint8_t)A->p2_bot;
+    s->bot_input[0] = (uint8_t)A->bot_in[0];
+    s->bot_input[1] = (uint8_t)A->bot_in[1];
   }
   return FS_OK;
 }
@@ -1322,26 +1367,29 @@ OR_EXPORT int or_get_state(or_handle C, fs_arena_state* out) {
    popping the inputs already consumed, and every FightState slot holds the previous call's
    state: getNextAIInput's ascending copy loop overwrites slots 1..9 with slot 0 before it
    reads slot 5 (AI:358-361), so slot 0 is all a later call can observe. */
-static void bot_set_state(arena_t* A, const fs_arena_state* s) {
-  bot_t* b = &A->bot;
-  memcpy(A->rng, s->rng, sizeof A->rng);
+static void bot_set_state(arena_t* A, int k, int32_t mp, int32_t mi, int32_t ap, int32_t ai, float pd, int32_t opp,
+                          int ready) {
+  bot_t* b = &A->bot[k];
   q_clear(&b->move_q);
   q_clear(&b->attack_q);
   b->move_plan = b->attack_plan = -1;
   b->move_len = b->attack_len = 0;
-  if (s->move_plan >= 0) {
-    set_move_plan(b, s->move_plan);
-    for (int i = 0; i < s->move_index && b->move_q.count > 0; i++) q_pop(&b->move_q);
+  if (mp >= 0) {
+    set_move_plan(b, k, mp);
+    for (int i = 0; i < mi && b->move_q.count > 0; i++) q_pop(&b->move_q);
   }
-  if (s->attack_plan >= 0) {
-    set_attack_plan(b, s->attack_plan);
-    for (int i = 0; i < s->attack_index && b->attack_q.count > 0; i++) q_pop(&b->attack_q);
+  if (ap >= 0) {
+    set_attack_plan(b, ap);
+    for (int i = 0; i < ai && b->attack_q.count > 0; i++) q_pop(&b->attack_q);
   }
   fight_state_t prev;
   memset(&prev, 0, sizeof prev);
-  const int opp = s->prev_opponent_action;
+  if (!ready) { /* fightStates all null: the next call answers 0 */
+    for (int i = 0; i < 10; i++) b->fs[i] = prev;
+    return;
+  }
   prev.valid = 1;
-  prev.distance_x = s->prev_distance;
+  prev.distance_x = pd;
   prev.opp_damage = opp == DAMAGE;
   prev.opp_guard_break = opp == GUARD_BREAK;
   prev.opp_blocking = opp == GUARD_CROUCH || opp == GUARD_STAND || opp == GUARD_M;
@@ -1391,12 +1439,19 @@ OR_EXPORT int or_set_state(or_handle C, const fs_arena_state* in) {
     A->rec_last[1] = s->recording_last[1];
     A->actor_in[0] = s->actor_input[0];
     A->actor_in[1] = s->actor_input[1];
+    A->bot_in[0] = s->bot_input[0];
+    A->bot_in[1] = s->bot_input[1];
+    A->p2_bot = s->p2_bot;
     A->reset_pending = s->reset_pending;
     A->has_terminated = s->has_terminated;
     A->cum_reward = s->cumulative_reward;
     A->round_state = s->reset_pending ? RS_KO : RS_FIGHT;
     A->timer = 0.0f;
-    if (C->cfg.p2_mode == FS_P2_BOT) bot_set_state(A, s);
+    memcpy(A->rng, s->rng, sizeof A->rng);
+    bot_set_state(A, 1, s->move_plan, s->move_index, s->attack_plan, s->attack_index, s->prev_distance,
+                  s->prev_opponent_action, s->bot_ready[1]);
+    bot_set_state(A, 0, s->p1_move_plan, s->p1_move_index, s->p1_attack_plan, s->p1_attack_index,
+                  s->p1_prev_distance, s->p1_prev_opponent_action, s->bot_ready[0]);
     A->cur_state = get_environment_state(A);
   }
   return FS_OK;

@@ -53,6 +53,13 @@ static bool same_arena(const fs_arena_state& a, const fs_arena_state& b, bool bo
     ok = ok && memcmp(a.rng, b.rng, 16) == 0 && a.move_plan == b.move_plan && a.move_index == b.move_index &&
          a.attack_plan == b.attack_plan && a.attack_index == b.attack_index &&
          memcmp(&a.prev_distance, &b.prev_distance, 4) == 0 && a.prev_opponent_action == b.prev_opponent_action;
+  // the actors (ABI 2): the game RNG is kept in every mode, the P1 bot's fields likewise
+  ok = ok && memcmp(a.rng, b.rng, 16) == 0 && memcmp(a.actor_input, b.actor_input, 2) == 0 &&
+       a.p2_bot == b.p2_bot && memcmp(a.bot_ready, b.bot_ready, 2) == 0 && memcmp(a.bot_input, b.bot_input, 2) == 0 &&
+       a.p1_move_plan == b.p1_move_plan && a.p1_move_index == b.p1_move_index &&
+       a.p1_attack_plan == b.p1_attack_plan && a.p1_attack_index == b.p1_attack_index &&
+       memcmp(&a.p1_prev_distance, &b.p1_prev_distance, 4) == 0 &&
+       a.p1_prev_opponent_action == b.p1_prev_opponent_action;
   return ok;
 }
 

@@ -31,7 +31,7 @@ class OracleBackend:
         assert self.o.set_state(st) == 0
 
     def set_p2_bot(self, bot):
-        raise NotImplementedError("the oracle handle's P2 mode is fixed")
+        assert self.o.set_p2_mode(_abi.FS_P2_BOT if bot else _abi.FS_P2_EXTERNAL) == 0
 
     def close(self):
         self.o.close()

@@ -54,11 +54,26 @@ LOOPING = {0, 1, 2, 350, 510}
 MOVE_PLAN_LEN, ATTACK_PLAN_LEN = [30, 90, 56, 70, 33, 60, 63], [30, 19, 23, 61, 121]
 
 
-def random_states(n, rng):
+def random_bot_fields(n, rng, prefix=""):
+    """Arbitrary queues mid-plan and FightState of one BattleAI (canonical fs_arena_state fields)."""
+    ids = np.array(sorted(ACTION_FRAMES), dtype=np.int32)
+    mp = rng.integers(-1, 7, n)
+    ap = rng.integers(-1, 5, n)
+    return {prefix + "move_plan": mp, prefix + "attack_plan": ap,
+            prefix + "move_index": np.where(mp < 0, 0, (rng.random(n) * np.take(MOVE_PLAN_LEN, np.maximum(mp, 0))).astype(int)),
+            prefix + "attack_index": np.where(ap < 0, 0, (rng.random(n) * np.take(ATTACK_PLAN_LEN,
+                                                                                   np.maximum(ap, 0))).astype(int)),
+            prefix + "prev_distance": rng.uniform(0.0, 9.0, n).astype(np.float32),
+            prefix + "prev_opponent_action": rng.choice(ids, n)}
+
+
+def random_states(n, rng, p2="external", p2_bot_frac=0.0):
     """Arbitrary loadable arena states (fs_arena_state), not only ones reachable from a reset:
     any action at any frame up to its frameCount, buffered / reserved actions, hitstun, latches,
     hasWon, saturated recordings, random histories and bot queues -- the paths a played match
-    reaches rarely (the hasWon request, reserve / buffer takes, DEAD past frame 63)."""
+    reaches rarely (the hasWon request, reserve / buffer takes, DEAD past frame 63).  The actors
+    fit the handle's P2 mode: a bot-created P2 is the bot and ready; with a remote P2 a fraction
+    `p2_bot_frac` of the arenas has the bot switched in (bot_ready random: a never-Reset bot)."""
     st = np.zeros(n, dtype=np.ctypeslib.as_array((_abi.fs_arena_state * 1)()).dtype)
     ids = np.array(sorted(ACTION_FRAMES), dtype=np.int32)
     for k in range(2):
@@ -84,12 +99,18 @@ def random_states(n, rng):
     st["actor_input"] = rng.integers(0, 8, (n, 2))
     st["cumulative_reward"] = rng.integers(-3, 4, n) * 0.3
     st["rng"] = rng.integers(1, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
-    mp = rng.integers(-1, 7, n)
-    ap = rng.integers(-1, 5, n)
-    st["move_plan"], st["attack_plan"] = mp, ap
-    st["move_index"] = np.where(mp < 0, 0, (rng.random(n) * np.take(MOVE_PLAN_LEN, np.maximum(mp, 0))).astype(int))
-    st["attack_index"] = np.where(ap < 0, 0,
-                                  (rng.random(n) * np.take(ATTACK_PLAN_LEN, np.maximum(ap, 0))).astype(int))
-    st["prev_distance"] = rng.uniform(0.0, 9.0, n).astype(np.float32)
-    st["prev_opponent_action"] = rng.choice(ids, n)
+    for k, v in {**random_bot_fields(n, rng), **random_bot_fields(n, rng, "p1_")}.items():
+        st[k] = v
+    st["bot_ready"] = rng.integers(0, 2, (n, 2))
+    st["bot_input"] = rng.integers(0, 8, (n, 2))
+    if p2 == "bot":
+        st["p2_bot"] = 1
+        st["bot_ready"][:, 1] = 1
+    elif p2 == "external":
+        st["p2_bot"] = (rng.random(n) < p2_bot_frac).astype(np.uint8)
+    # a bot that is not ready has no FightState: canonical zeros (STAND)
+    for k, pre in ((0, "p1_"), (1, "")):
+        idle = st["bot_ready"][:, k] == 0
+        st[pre + "prev_distance"][idle] = 0.0
+        st[pre + "prev_opponent_action"][idle] = 0
     return st

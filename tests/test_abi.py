@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "footsies.h")
 
 def declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fs_[a-z_]+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fs_[a-z_0-9]+)\(", text, re.M)))
 
 
 @pytest.fixture(scope="module")

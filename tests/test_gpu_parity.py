@@ -93,7 +93,7 @@ def test_lockstep_from_random_loaded_states(oracle_lib, p2):
     paths too (the oracle rebuilds the bot's real queues and FightState ring from the state)."""
     n = 4096
     sim, ora = make_pair(oracle_lib, n, p2, seed=21)
-    st = random_states(n, np.random.default_rng(77))
+    st = random_states(n, np.random.default_rng(77), p2=p2)
     assert ora.set_state(st) == 0
     sim.set_state(st)
     compare_states(ora.state(), sim.get_state(), step=-1)

@@ -8,20 +8,19 @@ from footsies_gym_amd import _abi
 from tests.parity_utils import random_states
 
 P2 = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT, "noop": _abi.FS_P2_NOOP}
-BOT_FIELDS = ("rng", "move_plan", "move_index", "attack_plan", "attack_index", "prev_distance",
-              "prev_opponent_action")
 
 
-@pytest.mark.parametrize("p2", sorted(P2))
-def test_oracle_state_roundtrip_and_determinism(oracle_lib, p2):
+@pytest.mark.parametrize("p2,p1_bot", [(p, False) for p in sorted(P2)] + [("external", True), ("bot", True)])
+def test_oracle_state_roundtrip_and_determinism(oracle_lib, p2, p1_bot):
     n = 1024
-    st = random_states(n, np.random.default_rng(5))
-    a = oracle_lib.Oracle(n, p2_mode=P2[p2], base_seed=1)
-    b = oracle_lib.Oracle(n, p2_mode=P2[p2], base_seed=2)
+    st = random_states(n, np.random.default_rng(5), p2=p2, p2_bot_frac=0.3)
+    p1m = _abi.FS_P1_BOT if p1_bot else _abi.FS_P1_EXTERNAL
+    a = oracle_lib.Oracle(n, p2_mode=P2[p2], base_seed=1, p1_mode=p1m)
+    b = oracle_lib.Oracle(n, p2_mode=P2[p2], base_seed=2, p1_mode=p1m)
     assert a.set_state(st) == 0 and b.set_state(st) == 0
     back = a.state()
     for name in st.dtype.names:
-        if name.startswith("pad") or (p2 != "bot" and name in BOT_FIELDS):
+        if name.startswith("pad"):
             continue
         if name == "f":
             for fn in st["f"].dtype.names:
