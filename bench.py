@@ -301,7 +301,9 @@ def main():
             raise SystemExit("--global-envs must be a multiple of the rank count")
         N = args.global_envs // world
     scaling = "strong" if args.global_envs else "weak"
-    sim = FootsiesSim(N, device=local, p2_mode="external", seed=rank * N)
+    # arena_base = the shard's first global index: seeds and the hashed action stream are those of
+    # the same arenas in one unsharded run (fs_config.arena_base), so every rank's work differs
+    sim = FootsiesSim(N, device=local, p2_mode="external", seed=0, arena_base=rank * N)
     h = sim.handle
     L = lib()
     # synthetic inputs resident in HBM before timing: W warm-up rows, then R regions of K rows
@@ -413,6 +415,17 @@ def main():
             if world > 1 and args.dist_backend == "nccl":
                 dist.all_gather_into_tensor(gbuf, rec)
     gwall = timed(run_step_gather, W, kg)
+
+    def run_step_gather_root(k0, n):  # the learner-only variant: grouped send / recv to rank 0
+        from footsies_gym_amd.parallel import gather_records_to
+        for k in range(k0, k0 + n):
+            rc = fs_step(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE)
+            rc = rc or fs_pack(h, C.c_void_p(rec.data_ptr()))
+            if rc:
+                check(rc, h)
+            if world > 1 and args.dist_backend == "nccl":
+                gather_records_to(rec, 0)
+    grwall = timed(run_step_gather_root, W, kg)
     # The dominant kernel of the reported mode, back-to-back launches.  The roofline block is
     # measured at a fixed launch shape (--roofline-ticks ticks per fs_step_n launch, the shape
     # the committed rocprofv3 summaries under profiles/ cover), independent of --steps; the
@@ -482,6 +495,10 @@ def main():
                              "bytes_gathered_per_step": world * N * _abi.FS_RECORD_BYTES,
                              "note": "fs_step + fs_pack_outputs + one all_gather_into_tensor of the 40-B "
                                      "(obs, reward, done) records over RCCL per step (none at 1 GPU or with --dist-backend gloo)"},
+        "step_gather_root_mode": {"value": world * N * kg / grwall, "ms_per_step": 1e3 * grwall / kg, "steps": kg,
+                                  "bytes_into_rank0_per_step": (world - 1) * N * _abi.FS_RECORD_BYTES,
+                                  "note": "fs_step + fs_pack_outputs + the records of every rank gathered to rank 0 "
+                                          "only (grouped send / recv over RCCL, parallel.gather_records_to)"},
     }
     if world == 1 and not args.no_extras:
         out["p2_bot_mode"] = bot_mode_rate(torch, N, K, W, chunk, args.seed, local)

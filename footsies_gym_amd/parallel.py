@@ -1,10 +1,12 @@
 """Multi-GPU: one process per GPU, arenas sharded by contiguous global index.
 
 Arenas are independent, so stepping needs no communication:
-rank r owns global arenas [r*N/G, (r+1)*N/G) and seeds its bots with the global
-index, so any G produces the same per-arena trajectories.  The only collective is
-the optional per-step gather of (obs, reward, done) for a centralised learner --
-one all_gather over RCCL/xGMI of a packed per-arena record (~30 B/arena).
+rank r owns global arenas [r*N/G, (r+1)*N/G); its handle's arena_base is r*N/G, so
+seeds, hashed actions and actor samples are keyed by the global index and any G
+produces the same per-arena trajectories.  The only collective is the optional
+per-step gather of (obs, reward, done) for a centralised learner: a packed 40-B
+per-arena record, all-gathered to every rank or gathered to one rank by grouped
+point-to-point sends over RCCL/xGMI.
 """
 import numpy as np
 
@@ -53,23 +55,59 @@ def unpack_outputs(rec, torch):
     }
 
 
+def _on_backend(t, group):
+    """gloo moves host tensors only: records of a device shard cross through host memory there
+    (the multi-rank rehearsal on one GPU); RCCL takes them where they are."""
+    import torch.distributed as dist
+    return t.cpu() if t.is_cuda and dist.get_backend(group) == "gloo" else t
+
+
 def gather_records(rec, group=None, shard_sizes=None):
     """All-gather every rank's packed [n, RECORD_BYTES] records into global-index order (one
     all_gather over RCCL/xGMI, or gloo on CPU).  `shard_sizes` (per rank) handles uneven shards
-    by padding to the largest.  Returns the [global_envs, RECORD_BYTES] records."""
+    by padding to the largest.  Returns the [global_envs, RECORD_BYTES] records on every rank."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     n = rec.shape[0]
     sizes = shard_sizes or [n] * world
     m = max(sizes)
+    dev = rec.device
+    rec = _on_backend(rec, group)
     if n < m:
         rec = torch.cat([rec, torch.zeros((m - n, RECORD_BYTES), dtype=rec.dtype, device=rec.device)])
     buf = torch.empty((world * m, RECORD_BYTES), dtype=rec.dtype, device=rec.device)
     dist.all_gather_into_tensor(buf, rec, group=group)
-    if all(sz == m for sz in sizes):
-        return buf
-    return torch.cat([buf[r * m: r * m + sizes[r]] for r in range(world)])
+    if not all(sz == m for sz in sizes):
+        buf = torch.cat([buf[r * m: r * m + sizes[r]] for r in range(world)])
+    return buf.to(dev)
+
+
+def gather_records_to(rec, dst=0, group=None, shard_sizes=None):
+    """Gather every rank's packed records to rank `dst` only (a centralised learner, SURVEY.md
+    §8(e)): one grouped point-to-point exchange -- each rank sends its shard, `dst` posts one
+    receive per peer straight into its slice of the global buffer (RCCL has no native gather; this
+    is the ncclGroupStart + ncclSend / ncclRecv pattern).  Each link carries one shard once, so
+    the traffic is (G-1)/G of what `gather_records`'s all_gather moves into every rank.  Returns
+    the [global_envs, RECORD_BYTES] records on `dst`, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = rec.shape[0]
+    sizes = shard_sizes or [n] * world
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+    dev = rec.device
+    rec = _on_backend(rec.contiguous(), group)
+    if rank != dst:
+        dist.send(rec, dst, group=group)
+        return None
+    out = torch.empty((int(starts[-1]), RECORD_BYTES), dtype=rec.dtype, device=rec.device)
+    out[starts[rank]:starts[rank + 1]] = rec
+    ops = [dist.P2POp(dist.irecv, out[starts[r]:starts[r + 1]], r, group=group) for r in range(world) if r != dst]
+    for w in dist.batch_isend_irecv(ops) if ops else []:
+        w.wait()
+    return out.to(dev)
 
 
 def gather_outputs(out, group=None, shard_sizes=None):
@@ -80,22 +118,32 @@ def gather_outputs(out, group=None, shard_sizes=None):
 
 
 class ShardedSim:
-    """This rank's FootsiesSim over its shard of `global_envs` arenas (global-index seeding)."""
+    """This rank's FootsiesSim over its shard of `global_envs` arenas.  The handle's arena_base is
+    the shard's first global index, so creation seeds, hashed actions and the in-kernel actor's
+    sampling stream are those of the same arenas in one unsharded run: results do not depend on G."""
 
     def __init__(self, global_envs, rank, world, device=0, seed=0, **kw):
         from .simulator import FootsiesSim
         self.start, self.stop = shard_range(global_envs, world, rank)
         self.sizes = [b - a for a, b in (shard_range(global_envs, world, r) for r in range(world))]
-        self.sim = FootsiesSim(self.stop - self.start, device=device, seed=seed + self.start, **kw)
+        self.sim = FootsiesSim(self.stop - self.start, device=device, seed=seed, arena_base=self.start, **kw)
 
     def step(self, p1, p2=None):
         return self.sim.step(p1, p2)
 
-    def gather(self, group=None):
-        """Every rank's outputs in global-index order: the records packed on device by
-        fs_pack_outputs, then one all_gather."""
+    def step_n(self, n, p1=None, p2=None, action_seed=0, trajectory=None):
+        return self.sim.step_n(n, p1, p2, action_seed=action_seed, trajectory=trajectory)
+
+    def gather(self, group=None, dst=None):
+        """The outputs of every rank in global-index order, packed on device by fs_pack_outputs:
+        on every rank (one all_gather, dst=None) or on rank `dst` only (grouped send / recv;
+        None on the other ranks)."""
         import torch
-        return unpack_outputs(gather_records(self.sim.pack_outputs(), group, self.sizes), torch)
+        rec = self.sim.pack_outputs()
+        if dst is None:
+            return unpack_outputs(gather_records(rec, group, self.sizes), torch)
+        g = gather_records_to(rec, dst, group, self.sizes)
+        return None if g is None else unpack_outputs(g, torch)
 
     def close(self):
         self.sim.close()

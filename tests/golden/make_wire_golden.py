@@ -6,8 +6,8 @@ The unmodified FootsiesEnv (imported from /root/reference with the throwaway gym
 stub) connects to FootsiesServer -- backed here by the CPU oracle, since this container
 has no GPU -- and plays scripted episodes through its public API: reset(seed=...),
 step(), mid-episode reset() (the RESET command), save_battle_state() /
-load_battle_state() and a custom opponent on the P2 port, with frame_delay on the
-client side.  The server records every message it receives and sends; the transcript
+load_battle_state(), a custom opponent on the P2 port, set_opponent() switching P2 between
+it and the in-game bot (the P2_BOT command), and frame_delay on the client side.  The server records every message it receives and sends; the transcript
 is the fixture: tests replay the client half against the GPU-backed server and require
 the server half back byte for byte.  Output (committed): tests/golden/wire_golden.json.gz.
 """
@@ -33,7 +33,7 @@ from oracle import binding  # noqa: E402
 from tests.oracle_server_backend import OracleBackend  # noqa: E402
 
 
-def play(name, opponent, frame_delay, steps, seed, rng_seed):
+def play(name, opponent, frame_delay, steps, seed, rng_seed, switch_every=0):
     transcript = []
     remote_p2 = opponent is not None
     srv = FootsiesServer("127.0.0.1", 0, 0, 0 if remote_p2 else None, p2_no_state=True,
@@ -63,6 +63,8 @@ def play(name, opponent, frame_delay, steps, seed, rng_seed):
             saved = env.save_battle_state()
         elif remote_p2 and saved is not None and t % 61 == 40:
             env.load_battle_state(saved)
+        if switch_every and t % switch_every == switch_every - 1:  # FE:458-480: P2_BOT both ways
+            env.set_opponent(None if env.opponent is not None else opponent)
     env.close() if hasattr(env, "close") else None
     for s in (env.comm, env.remote_control_comm, env.opponent_comm):
         if s is not None:
@@ -79,6 +81,7 @@ def main():
     cases = {
         "bot": play("bot", None, 0, 2500, 3, 1),
         "remote_delay2": play("remote_delay2", opp, 2, 2500, 4, 2),
+        "remote_switch": play("remote_switch", opp, 0, 2500, 5, 3, switch_every=113),
     }
     with gzip.open(os.path.join(HERE, "wire_golden.json.gz"), "wt") as f:
         json.dump(cases, f)

@@ -8,6 +8,7 @@ from footsies_gym_amd import _abi
 
 class OracleBackend:
     def __init__(self, oracle_lib, p2_bot=True, seed=0):
+        self.remote = not p2_bot
         self.o = oracle_lib.Oracle(1, p2_mode=_abi.FS_P2_BOT if p2_bot else _abi.FS_P2_EXTERNAL,
                                    autoreset_mode=_abi.FS_AUTORESET_NEXT_STEP, base_seed=seed)
 
@@ -15,6 +16,8 @@ class OracleBackend:
         return self.o.env_state()[0]
 
     def step(self, p1, p2):
+        if p2 is None and self.remote:  # the handle's remote P2 is switched to the bot: no action arrived
+            p2 = 0
         out = self.o.step(np.array([p1], np.uint8), None if p2 is None else np.array([p2], np.uint8))
         return bool(out["terminated"][0])
 

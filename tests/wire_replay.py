@@ -10,7 +10,7 @@ from footsies_gym_amd.server import FootsiesServer
 from tests import wire_client
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CASES = ("bot", "remote_delay2")
+CASES = ("bot", "remote_delay2", "remote_switch")
 _CACHE = {}
 
 
