@@ -1154,7 +1154,35 @@ __device__ __forceinline__ uint32_t hash_action(uint64_t seed, uint64_t env, uin
 // tick to be acknowledged by memory.
 __device__ __forceinline__ void settle(uint32_t& next) { asm volatile("" : "+v"(next)); }
 
-template <int FM, int P2>
+// The fused loop's action rows, two ticks ahead, as loads the compiler does not track.  With the
+// compiler's own load the row for tick t+1 had to be resident before tick t's stores, a wait that
+// also drained tick t-1's stores (gfx9 counts loads and stores on one in-order vmcnt) and left one
+// tick to cover the load.  Here the row for tick t+1 is issued at the top of tick t-1, and before
+// tick t's stores the wave waits with vmcnt(11): at least 11 vector memory ops were issued after
+// that load -- tick t-1's output stores (10 on every path of env_step: write_main's 7 plus reward,
+// terminated, truncated) and tick t+2's load -- so the row is resident while those stores may
+// still be in flight.  The loaded register is read by nothing but the wait statement, which copies
+// the row out after the s_waitcnt; tools/check_async_loads.py checks on the assembly that no
+// instruction touches a register between its load and its wait (tests/test_async_loads.py).
+__device__ __forceinline__ uint32_t row_load(const uint8_t* p) {
+  uint32_t v;
+  asm volatile("global_load_ubyte %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <int WAIT>
+__device__ __forceinline__ void settle_w(uint32_t& next) {
+  if constexpr (WAIT < 0) {
+    asm volatile("" : "+v"(next));
+  } else {
+    // the in-flight register is read only by this statement, after the wait; the value the next
+    // tick uses is a fresh register written here
+    uint32_t ready;
+    asm volatile("s_waitcnt vmcnt(%2)\n\tv_mov_b32 %0, %1" : "=v"(ready) : "v"(next), "n"(WAIT) : "memory");
+    next = ready;
+  }
+}
+
+template <int FM, int P2, int WAIT = -1>
 __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   const DevOutputs& o = p.out;
@@ -1166,7 +1194,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.has_term = false;
     L.cum = 0.0;
     L.ai = action_info(L.f.act);
-    settle(next);
+    settle_w<WAIT>(next);
     write_main(L, o, r);
     st_off(o.reward, 8 * r, 0.0);  // per-arena outputs: both lanes store the same value (no divergent branch)
     st_off(o.terminated, r, (uint8_t)0);
@@ -1239,7 +1267,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     const uint32_t fl2 = k == 0 ? o_fl : my_fl;
     reward = over ? ((fl2 & 1u) ? 1.0 : -1.0) : 0.0;
   }
-  settle(next);
+  settle_w<WAIT>(next);
   if (over) {
     L.f.hist = 0;  // ChangeRoundState(KO): ClearInput (BC:296-299)
     L.f.hold = 0;
@@ -1316,7 +1344,9 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   // the arena state and the first action are in flight while the block stages the tables
   Lane L;
   load_lane<P2>(L, p.st, a, k);
-  uint32_t next = fetch(0);
+  uint32_t next;
+  if constexpr (FUSED && !HASH && !POL) next = row_load((reads ? src : p.p1) + (uint32_t)a);
+  else next = fetch(0);
   if constexpr (POL) stage_policy(p.pol);
   stage_tables();
   if constexpr (POL) {
@@ -1349,10 +1379,44 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     }
   } else if constexpr (FUSED) {
     const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
-    for (int t = 0; t < p.n_steps; t++) {
-      const uint32_t act = next;
-      next = fetch(min(t + 1, p.n_steps - 1));  // the last tick re-reads its own row
-      env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
+    if constexpr (HASH) {
+      for (int t = 0; t < p.n_steps; t++) {
+        const uint32_t act = next;
+        next = fetch(min(t + 1, p.n_steps - 1));
+        env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
+      }
+    } else {
+      // Rows two ticks ahead, loaded and waited for as described at row_load, in two registers
+      // that swap roles every tick (unrolled by two, so no register copy of a row in flight).
+      // *_fl: a load in flight (read only by its wait), *_rd: the row once resident.  A load is
+      // issued every tick (the last rows re-read the last one) so the wait counts hold, and the
+      // last one in flight is waited for before the wave ends.
+      const int last = p.n_steps - 1;
+      // every lane loads (so the in-flight register is written by the load alone); a lane without a
+      // row of its own reads P1's row 0, always valid in these launches, and ignores it
+      const uint8_t* own = reads ? src : p.p1;
+      const uint32_t row_mul = reads ? (uint32_t)p.n_envs : 0u;
+      auto issue = [&](int t) -> uint32_t {
+        return row_load(own + (uint32_t)min(t, last) * row_mul + (uint32_t)a);
+      };
+      uint32_t a_fl = next, b_fl = issue(1), a_rd, b_rd;
+      asm volatile("s_waitcnt vmcnt(0)\n\tv_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(a_rd), "=v"(b_rd)
+                   : "v"(a_fl), "v"(b_fl) : "memory");
+      int t = 0;
+      for (; t < last; t += 2) {
+        a_fl = issue(t + 2);
+        env_step<FM, P2, 11>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
+        b_rd = b_fl;
+        b_fl = issue(t + 3);
+        env_step<FM, P2, 11>(L, reads ? b_rd & 7u : 0u, p, (uint32_t)(t + 1) * row_step + (uint32_t)a, a_fl);
+        a_rd = a_fl;
+      }
+      if (t == last) {  // an odd tick count: the last tick waits for a re-read of the last row
+        a_fl = issue(t + 2);
+        uint32_t b_last = b_fl;  // (b_fl itself stays the in-flight value for the final wait)
+        env_step<FM, P2, 11>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_last);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::"v"(a_fl), "v"(b_fl) : "memory");  // no load outlives the wave
     }
   } else {
     uint32_t none = 0;
