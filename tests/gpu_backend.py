@@ -23,6 +23,12 @@ class SimBackend:
     def env_state(self):
         return self.sim.env_state()
 
+    def state(self):
+        return self.sim.get_state()
+
+    def set_state(self, st):
+        self.sim.set_state(st)
+
 
 def make(n, p2_mode, dense, autoreset, seed, frame_delay=0):
     return SimBackend(n, p2_mode, dense, autoreset, seed, frame_delay)

@@ -5,6 +5,7 @@ import pytest
 
 from footsies_gym_amd import _abi
 from tests import golden_utils as gu
+from tests import kat_combat
 from tests import kat_scenarios as kat
 from tests import wire_client, wire_replay
 from tests import wrapper_replay as wr
@@ -17,6 +18,11 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(kat.ALL))
 def test_kat_gpu(name):
     kat.ALL[name](SimBackend(1))
+
+
+@pytest.mark.parametrize("name", sorted(kat_combat.ALL))
+def test_kat_combat_gpu(name):
+    kat_combat.ALL[name](SimBackend(1))
 
 
 @pytest.mark.parametrize("name", gu.CASES)

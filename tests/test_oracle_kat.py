@@ -2,7 +2,7 @@
 import pytest
 
 from footsies_gym_amd import _abi
-from tests import kat_actors
+from tests import kat_actors, kat_combat
 from tests import kat_scenarios as kat
 
 
@@ -15,3 +15,8 @@ def test_kat_oracle(oracle_lib, name):
 @pytest.mark.parametrize("name", sorted(kat_actors.ALL))
 def test_kat_actors_oracle(oracle_lib, name):
     kat_actors.ALL[name](lambda p1, p2, seed: kat_actors.OracleActors(oracle_lib, p1, p2, seed))
+
+
+@pytest.mark.parametrize("name", sorted(kat_combat.ALL))
+def test_kat_combat_oracle(oracle_lib, name):
+    kat_combat.ALL[name](kat_combat.OracleKat(oracle_lib))
