@@ -73,7 +73,7 @@ struct Fighter {
   // the fighter their world x (y == rect.y since position.y is always 0)
   int rec;        // FrameRec index of (action, frame)
   float px, ux0, ux1, hx0, hx1;
-  float pw, pymin, pymax;  // pushbox width, yMin, yMax of the record
+  float pw;       // pushbox width of the record
 };
 
 struct Arena {
@@ -264,6 +264,14 @@ __device__ __forceinline__ void set_action(Fighter& f, int a) {  // SetCurrentAc
 // between two struct values (HIP's uint4 included) would go through scratch memory.
 typedef uint32_t AInfo __attribute__((ext_vector_type(4)));  // a native vector: selects stay in registers
 __device__ __forceinline__ AInfo action_info(int a) { return reinterpret_cast<const AInfo*>(sT.action)[a]; }
+__device__ __forceinline__ AInfo stand_info() {  // action_info(A_STAND), as constants
+  AInfo i;
+  i.x = kStandInfo[0];
+  i.y = kStandInfo[1];
+  i.z = kStandInfo[2];
+  i.w = kStandInfo[3];
+  return i;
+}
 __device__ __forceinline__ int ai_frame_count(AInfo i) { return (int)(int16_t)(i.x & 0xffffu); }
 __device__ __forceinline__ int ai_loop_from(AInfo i) { return (int)(int16_t)(i.x >> 16); }
 __device__ __forceinline__ bool ai_always_cancel(AInfo i) { return (i.y & 0xffu) != 0; }
@@ -349,7 +357,10 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   const bool ended = f.frame >= ai_frame_count(ai);
   const bool inwin = (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai));
   const uint32_t cls = ended ? 2u : (inwin ? 1u : 0u);
-  const uint32_t idx = ((uint32_t)f.act << 8) | ((9u * cls + 3u * e.atk + e.dash) << 3) | (e.held << 1) | (uint32_t)f.prox;
+  // (the low five bits XOR-swizzled with the action, as tools/gen_tables.py lays the table out:
+  // lanes that differ in action but not in inputs read different LDS banks)
+  const uint32_t in8 = ((9u * cls + 3u * e.atk + e.dash) << 3) | (e.held << 1) | (uint32_t)f.prox;
+  const uint32_t idx = ((uint32_t)f.act << 8) | (in8 ^ (uint32_t)f.act);
   const uint32_t q = sT.req_table[early ? (uint32_t)(kReqEarly + a0) : idx];
   const bool set = ((q >> 11) & 1u) != 0;  // SetCurrentAction ran (F:546-563)
   const bool bset = ((q >> 10) & 1u) != 0;
@@ -377,13 +388,27 @@ __device__ __forceinline__ void update_movement(Fighter& f, float v) {
   f.x = (f.stun <= 0 && v != 0.0f) ? nx : f.x;
 }
 
-// Frame record `rec` of facing `k` in LDS.  The byte offset is formed with 24-bit multiplies
-// (v_mul_u32_u24, full rate): indexing sT.recs[k][rec] directly makes a 64-bit v_mad_u64_u32
-// and a v_mul_lo_u32, both quarter-rate, on the dependency chain of every tick.
-__device__ __forceinline__ const FrameRec& frame_rec(uint32_t k, uint32_t rec) {
-  const char* base = reinterpret_cast<const char*>(&sT.recs[0][0]);
-  return *reinterpret_cast<const FrameRec*>(base + __umul24(k, (uint32_t)sizeof(sT.recs[0])) +
-                                            __umul24(rec, (uint32_t)sizeof(FrameRec)));
+// The frame record `rec` of facing `k` in LDS (fs_tables.h: rec_push / rec_hurt / rec_hit, one
+// 16-B entry each).  The byte offset is formed with 24-bit multiplies (v_mul_u32_u24, full rate):
+// indexing the arrays directly makes a 64-bit v_mad_u64_u32 and a v_mul_lo_u32, both quarter-rate,
+// on the dependency chain of every tick.
+typedef float F4 __attribute__((ext_vector_type(4)));     // native vectors: they stay in registers
+typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+struct RecGeo {
+  F4 push;  // pushbox x offset, width, velocity, 0
+  F4 hurt;  // hurtbox 0 (x offset, width / 2), hurtbox 1
+  F4 hit;   // hitbox 0 (x offset, width / 2), hitbox 1
+};
+__device__ __forceinline__ RecGeo frame_rec(uint32_t k, uint32_t rec) {
+  const uint32_t off = __umul24(k, (uint32_t)sizeof(sT.rec_push[0])) + __umul24(rec, 16u);
+  auto at = [&](const void* base) {
+    return *reinterpret_cast<const F4*>(reinterpret_cast<const char*>(base) + off);
+  };
+  RecGeo g;
+  g.push = at(&sT.rec_push[0][0]);
+  g.hurt = at(&sT.rec_hurt[0][0]);
+  g.hit = at(&sT.rec_hit[0][0]);
+  return g;
 }
 
 // the frame record of (act, frame)
@@ -394,15 +419,13 @@ __device__ __forceinline__ int frame_record(const Fighter& f) {
 // UpdateBoxes (F:671-697): world x of every box of the record, `R` being the record in
 // the fighter's facing (x offsets pre-signed): basePosition.x + dataRect.x * sign.
 template <int FM>
-__device__ __forceinline__ void update_boxes(Fighter& f, const FrameRec& R) {
+__device__ __forceinline__ void update_boxes(Fighter& f, const RecGeo& R) {
   f.pw = R.push.y;
-  f.pymin = R.push.z;
-  f.pymax = R.push.w;
   f.px = fadd<FM>(f.x, R.push.x);
-  f.ux0 = fadd<FM>(f.x, R.hurt[0].x);
-  f.ux1 = fadd<FM>(f.x, R.hurt[1].x);
-  f.hx0 = fadd<FM>(f.x, R.hit[0].x);
-  f.hx1 = fadd<FM>(f.x, R.hit[1].x);
+  f.ux0 = fadd<FM>(f.x, R.hurt.x);
+  f.ux1 = fadd<FM>(f.x, R.hurt.z);
+  f.hx0 = fadd<FM>(f.x, R.hit.x);
+  f.hx1 = fadd<FM>(f.x, R.hit.z);
 }
 
 // ApplyPositionChange (F:331-350): position and every box are shifted, not rebuilt
@@ -431,8 +454,6 @@ __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
 
 // BoxBase (F:8-26): boxes are (world x, width/2, yMin, yMax); xMin = x - w/2, xMax = x + w/2
 // (F:12-13) and Overlaps is inclusive.  The hit test below evaluates it per box pair.
-typedef float Box4 __attribute__((ext_vector_type(4)));  // (x offset, width/2, yMin, yMax) in registers
-__device__ __forceinline__ Box4 box4(const float4& b) { return *reinterpret_cast<const Box4*>(&b); }
 
 constexpr int DR_DAMAGE = 1, DR_GUARD = 2, DR_GUARD_BREAK = 3;
 
@@ -446,7 +467,7 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
       f.guard = 0;
     }
   }
-  if (f.act == A_BACKWARD || sT.action[f.act].guard_type) {
+  if (f.act == A_BACKWARD || ((kGuardTypeMask >> f.act) & 1u)) {
     set_action(f, ad.guard_action);
     if (guard_break) {
       f.rsv = A_GUARD_BREAK;
@@ -476,12 +497,12 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
 // only) and comes from kTables.ybits, which is also 0 for absent boxes (past a record's box
 // count), so no count checks are needed here.
 template <int FM>
-__device__ __forceinline__ uint32_t box_x_overlaps(Box4 h0, Box4 h1, float hx0, float hx1, Box4 u0, Box4 u1,
+__device__ __forceinline__ uint32_t box_x_overlaps(float hw0, float hw1, float hx0, float hx1, float uw0, float uw1,
                                                    float ux0, float ux1) {
-  const float h0min = fsub<FM>(hx0, h0.y), h0max = fadd<FM>(hx0, h0.y);
-  const float h1min = fsub<FM>(hx1, h1.y), h1max = fadd<FM>(hx1, h1.y);
-  const float u0min = fsub<FM>(ux0, u0.y), u0max = fadd<FM>(ux0, u0.y);
-  const float u1min = fsub<FM>(ux1, u1.y), u1max = fadd<FM>(ux1, u1.y);
+  const float h0min = fsub<FM>(hx0, hw0), h0max = fadd<FM>(hx0, hw0);
+  const float h1min = fsub<FM>(hx1, hw1), h1max = fadd<FM>(hx1, hw1);
+  const float u0min = fsub<FM>(ux0, uw0), u0max = fadd<FM>(ux0, uw0);
+  const float u1min = fsub<FM>(ux1, uw1), u1max = fadd<FM>(ux1, uw1);
   auto ov = [](float smin, float smax, float omin, float omax) {
     return (uint32_t)((omax >= smin) & (omin <= smax));
   };
@@ -879,19 +900,16 @@ __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int
 
 // UpdatePushCharacterVsCharacter (BC:483-501) with UnityEngine.Rect semantics:
 // x is xMin, xMax = width + x, Overlaps is strict; each lane applies its own fighter's
-// shift.  The y-test is dropped when tools/gen_tables.py proves every pair of pushboxes
-// overlaps vertically (kPushYAlwaysOverlaps).
+// shift.  The y-test is constant: tools/gen_tables.py proves every pair of pushboxes
+// overlaps vertically (kPushYAlwaysOverlaps) and keeps no y extents in the records.
+static_assert(kPushYAlwaysOverlaps, "the frame records keep no pushbox y extents");
 template <int FM>
 __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t k) {
   // The test and the shift are symmetric in the two fighters, so each lane evaluates them
   // as (mine, partner's) -- the same operations on the same values as (P1, P2).
   const float o_px = xpair(f.px), o_x = xpair(f.x), o_pw = xpair(f.pw);
   const float xmax_m = fadd<FM>(f.pw, f.px), xmax_o = fadd<FM>(o_pw, o_px);  // Rect.xMax = width + x
-  bool overlap = (xmax_o > f.px) & (o_px < xmax_m);
-  if constexpr (!kPushYAlwaysOverlaps) {  // record pushboxes are (x offset, width, yMin, yMax)
-    const float o_ymin = xpair(f.pymin), o_ymax = xpair(f.pymax);
-    overlap = overlap & (o_ymax > f.pymin) & (o_ymin < f.pymax);
-  }
+  const bool overlap = (xmax_o > f.px) & (o_px < xmax_m);
   if (!overlap || f.x == o_x) return;  // a tie pushes nothing (BC:490-499)
   const bool left = f.x < o_x;         // the left fighter moves by -d/2, the right one by +d/2
   float dx;
@@ -917,28 +935,62 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
 // the frame record (one round trip) rather than here.
 __device__ __forceinline__ uint32_t bit0_mask(uint32_t v) { return (uint32_t)((int32_t)(v << 31) >> 31); }  // 0 / ~0
 
+// AttackData of attack index i (kAttacks, fs_tables.h) selected in registers: the hit path
+// makes no LDS round trip for it.
+constexpr uint32_t attack_word(int j, int w) {
+  return w == 0 ? (uint32_t)kAttacks[j].damage_action | ((uint32_t)kAttacks[j].guard_action << 8) |
+                      ((uint32_t)kAttacks[j].number_of_hit << 16) | ((uint32_t)kAttacks[j].vital_damage << 24)
+                : (uint32_t)kAttacks[j].guard_damage | ((uint32_t)kAttacks[j].hit_stun << 8) |
+                      ((uint32_t)kAttacks[j].guard_stun << 16) | ((uint32_t)kAttacks[j].guard_break_stun << 24);
+}
+template <int W>
+__device__ __forceinline__ uint32_t attack_word_sel(bool b1, bool b2) {
+  constexpr uint32_t a0 = attack_word(0, W), a1 = attack_word(1, W), a2 = attack_word(2, W), a3 = attack_word(3, W);
+  return b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
+}
+__device__ __forceinline__ AttackInfo attack_info(int i) {
+  static_assert(sizeof(AttackInfo) == 8, "AttackInfo is two words");
+  static_assert(sizeof(kAttacks) / sizeof(kAttacks[0]) == 4, "four attacks");
+  const bool b1 = i & 1, b2 = i & 2;
+  const uint32_t w[2] = {attack_word_sel<0>(b1, b2), attack_word_sel<1>(b1, b2)};
+  AttackInfo a;
+  a.damage_action = (uint8_t)w[0];
+  a.guard_action = (uint8_t)(w[0] >> 8);
+  a.number_of_hit = (uint8_t)(w[0] >> 16);
+  a.vital_damage = (uint8_t)(w[0] >> 24);
+  a.guard_damage = (uint8_t)w[1];
+  a.hit_stun = (uint8_t)(w[1] >> 8);
+  a.guard_stun = (uint8_t)(w[1] >> 16);
+  a.guard_break_stun = (uint8_t)(w[1] >> 24);
+  return a;
+}
+
+// `res` = kTables.resolve[o_rec * 4 + o_hits], read with the frame record: byte m (the box-pair
+// overlap mask) holds the outcome at the attacker's hit count o_hits (low nibble) and at 0 (high).
 template <int FM>
-__device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, Box4 my_hurt0, Box4 my_hurt1,
-                                                         Box4 their_hit0, Box4 their_hit1, uint32_t o_rec,
-                                                         uint32_t ym) {
-  // (no wave-level skip: absent hitboxes have empty y-extents and never overlap)
-  const int o_hits = xpair(f.hits);
+__device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, F4 my_hurt, float o_hw0, float o_hw1,
+                                                         U4 res, uint32_t ym) {
+  // (no wave-level skip: absent hitboxes never overlap in y, ybits)
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
-  const uint32_t xm = box_x_overlaps<FM>(their_hit0, their_hit1, o_hx0, o_hx1, my_hurt0, my_hurt1, f.ux0, f.ux1);
+  const uint32_t xm = box_x_overlaps<FM>(o_hw0, o_hw1, o_hx0, o_hx1, my_hurt.y, my_hurt.w, f.ux0, f.ux1);
   // phase A (P1 attacks P2) is resolved on the P2 lane; its outcome crosses to P1, whose lane
   // then resolves phase B (P2 attacks P1) with P2's hit count after phase A
-  // the resolution for both phases from one table entry of the attacker's record
-  // (kTables.resolve, tools/gen_tables.py): nibble h = the outcome at attacker hit count h
-  const uint32_t tab = sT.resolve[(o_rec << 4) | (xm & ym)];
-  // The entry shifted by the partner's hit count: on the P2 lane phase A's outcome (P1's hit
-  // count); on the P1 lane phase B's, unless phase A hit P2 -- which resets P2's hit count to 0
-  // first (SetCurrentAction), so P1 then reads nibble 0.
+  // the resolution for both phases from one byte of the attacker's entry (kTables.resolve,
+  // tools/gen_tables.py), picked by v_perm_b32 (selector byte m & 7 of the low or high 8 bytes;
+  // selector 0x0c = zero)
+  const uint32_t m = xm & ym;
+  const uint32_t sel = (m & 7u) | 0x0c0c0c00u;
+  const uint32_t lo = __builtin_amdgcn_perm(res.y, res.x, sel), hi = __builtin_amdgcn_perm(res.w, res.z, sel);
+  const uint32_t tab = (m & 8u) ? hi : lo;
+  // On the P2 lane phase A's outcome (at P1's hit count); on the P1 lane phase B's, unless phase
+  // A hit P2 -- which resets P2's hit count to 0 first (SetCurrentAction), so P1 then reads the
+  // outcome at hit count 0.
   // (every exchange is its own statement on both lanes: inside a select the compiler may run
   // the DPP move under a one-lane exec mask, and a disabled source lane reads as 0)
-  const uint32_t t1 = tab >> (4u * (uint32_t)o_hits);
+  const uint32_t t1 = tab & 15u;
   const uint32_t x1 = xpair(t1);
   const uint32_t hitA = (k == 1 ? t1 : x1) & 1u;
-  const uint32_t t = (k == 0 && hitA) ? tab : t1;  // this lane's phase as the defender
+  const uint32_t t = (k == 0 && hitA) ? (tab >> 4) : t1;  // this lane's phase as the defender
   const bool my_hit = (t & 1u) != 0;
   const int my_atk = (int)((t >> 1) & 3u);
   const bool my_prox = ((t >> 3) & 1u) != 0;
@@ -948,7 +1000,7 @@ __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k,
   f.hits += k == 0 ? (int)hitA : 0;  // NotifyAttackHit for P1 (F:352-355)
   int my_stun = 0;
   if (my_hit) {
-    const AttackInfo ad = sT.attacks[my_atk];
+    const AttackInfo ad = attack_info(my_atk);
     const int res = notify_damaged(f, ad);
     my_stun = res == DR_GUARD ? ad.guard_stun : res == DR_GUARD_BREAK ? ad.guard_break_stun : ad.hit_stun;
   }
@@ -1193,7 +1245,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.pending = false;
     L.has_term = false;
     L.cum = 0.0;
-    L.ai = action_info(L.f.act);
+    L.ai = stand_info();  // the burst ends on STAND
     settle_w<WAIT>(next);
     write_main(L, o, r);
     st_off(o.reward, 8 * r, 0.0);  // per-arena outputs: both lanes store the same value (no divergent branch)
@@ -1228,23 +1280,31 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   uint32_t rec_set;
   const bool set = update_action_request(L.f, e, ai, &rec_set);
   L.f.rec = set ? (int)rec_set : rec_cont;
-  const FrameRec& R = frame_rec(k, (uint32_t)L.f.rec);
-  // the collision's boxes: mine and the partner's (its record index crosses the pair now)
-  const int o_rec = xpair(L.f.rec);
-  const Box4 my_hurt0 = box4(R.hurt[0]), my_hurt1 = box4(R.hurt[1]);
-  const FrameRec& O = frame_rec(0, (uint32_t)o_rec);
-  const Box4 their_hit0 = box4(O.hit[0]), their_hit1 = box4(O.hit[1]);
-  // the y half of the box-pair overlaps (records only, kTables.ybits)
+  // One LDS round trip for everything the rest of the tick reads from the tables: my frame
+  // record, the y half of the box-pair overlaps (records only, kTables.ybits) and the hit
+  // resolution of the partner's record at its hit count (the record index and the hit count
+  // cross the pair first).
+  const RecGeo R = frame_rec(k, (uint32_t)L.f.rec);
+  const uint32_t o_rec = (uint32_t)xpair(L.f.rec);
+  const uint32_t o_hits = (uint32_t)xpair(L.f.hits);
   static_assert(kNumFrameRecs <= 64, "ybits rows are 64 records wide");
-  const uint32_t ym = sT.ybits[((uint32_t)o_rec << 6) | (uint32_t)L.f.rec];
-  update_movement<FM>(L.f, R.vel);
+  const uint32_t ym = sT.ybits[(o_rec << 6) | (uint32_t)L.f.rec];
+  const U4 res = reinterpret_cast<const U4*>(sT.resolve)[(o_rec << 2) | o_hits];
+  update_movement<FM>(L.f, R.push.z);
   update_boxes<FM>(L.f, R);
+  // the partner's hitbox half-widths (its own record's)
+  const float o_hw0 = xpair(R.hit.y), o_hw1 = xpair(R.hit.w);
   push_character_vs_character<FM>(L.f, k);
   push_character_vs_background<FM>(L.f);
   // consumed here, unconditionally, so the reads stay where they were issued (next to the
   // frame record) instead of being sunk into the collision's branch
-  asm volatile("" ::"v"(my_hurt0), "v"(my_hurt1), "v"(their_hit0), "v"(their_hit1), "v"(ym));
-  hitbox_hurtbox_collision<FM>(L.f, k, my_hurt0, my_hurt1, their_hit0, their_hit1, (uint32_t)o_rec, ym);
+  // (R.push too: its fourth word is unused, and a register of a load in flight that the
+  // allocator considers free is reused at once, which forces a wait for the load)
+  asm volatile("" ::"v"(R.push), "v"(R.hurt), "v"(o_hw0), "v"(o_hw1), "v"(res), "v"(ym));
+  hitbox_hurtbox_collision<FM>(L.f, k, R.hurt, o_hw0, o_hw1, res, ym);
+  // the next tick's ActionInfo, issued now so its LDS latency hides behind the KO test, the
+  // reward and the stores (only the reset paths below change the action again: to STAND)
+  const AInfo ai_next = action_info(L.f.act);
   // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes: each
   // lane's flags (bit 0: vital 0, bit 1: guard dropped this tick; both fields are 0..3) cross
   // the pair once, then fl1 / fl2 are P1's / P2's
@@ -1301,7 +1361,10 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   st_off(o.reward, 8 * r, reward);  // identical on both lanes of the arena
   st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
   st_off(o.truncated, r, (uint8_t)0);
-  L.ai = action_info(L.f.act);  // for the next tick (hits and resets set actions too)
+  // all four words live until here (the tick reads three; see R.push above)
+  asm volatile("" ::"v"(ai_next));
+  // for the next tick: a same-step reset burst ended on STAND
+  L.ai = (over && p.autoreset_mode == FS_AUTORESET_SAME_STEP) ? stand_info() : ai_next;
 }
 
 // P1's observation features for the in-kernel actor (fs_policy.h), packed bf16x2:
