@@ -55,6 +55,7 @@ struct fs_context {
   uint8_t* h_mask = nullptr;     // pinned [N]
   hipEvent_t staging_free = nullptr;
   uint4* delay_ring = nullptr;   // frame_delay > 0: [d][N] x 32-B observation records (fs_delay.hip)
+  uint8_t* delay_head = nullptr; // frame_delay > 0: [N] each arena's ring head
   std::vector<uint8_t> p2bot;    // host mirror of each arena's P2 actor (1 = the bot)
   int p2bot_count = 0;
   std::vector<void*> allocations;
@@ -132,7 +133,8 @@ void outputs_from_own(fs_context* h) {
 }
 
 // FootsiesEnv's delayed-frame queue over rows the last kernel wrote (no-op for frame_delay 0)
-int apply_delay(fs_context* h, const fsk::DevOutputs& out, int n_steps, int stride, bool refill_only) {
+int apply_delay(fs_context* h, const fsk::DevOutputs& out, int n_steps, int stride, bool refill_only,
+                const uint8_t* active = nullptr) {
   if (h->cfg.frame_delay <= 0) return FS_OK;
   fsk::DelayParams dp{};
   dp.out = out;
@@ -141,7 +143,8 @@ int apply_delay(fs_context* h, const fsk::DevOutputs& out, int n_steps, int stri
   dp.delay = h->cfg.frame_delay;
   dp.n_steps = n_steps;
   dp.out_stride_steps = stride;
-  dp.step0 = h->steps;
+  dp.head = h->delay_head;
+  dp.active = active;
   dp.refill_only = refill_only ? 1 : 0;
   dp.same_step = h->cfg.autoreset_mode == FS_AUTORESET_SAME_STEP;
   HIP_TRY(h, fsk::launch_delay(dp, h->stream));
@@ -223,7 +226,11 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   // staging
   if ((rc = dalloc(h, &h->d_act, 2 * N)) || (rc = dalloc(h, &h->d_seeds, N)) || (rc = dalloc(h, &h->d_mask, N)))
     return fail(rc);
-  if (cfg->frame_delay > 0 && (rc = dalloc(h, &h->delay_ring, 2 * (size_t)cfg->frame_delay * N))) return fail(rc);
+  if (cfg->frame_delay > 0 && ((rc = dalloc(h, &h->delay_ring, 2 * (size_t)cfg->frame_delay * N)) ||
+                               (rc = dalloc(h, &h->delay_head, N))))
+    return fail(rc);
+  if (cfg->frame_delay > 0 && hipMemsetAsync(h->delay_head, 0, N, h->stream) != hipSuccess)
+    return fail(set_err(h, FS_E_DEVICE, "memset"));
   if (hipHostMalloc((void**)&h->h_act, 2 * N, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&h->h_seeds, N * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&h->h_mask, N, hipHostMallocDefault) != hipSuccess)
@@ -364,7 +371,7 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
     return FS_OK;
   }
   HIP_TRY(h, fsk::launch_step(sp, h->cfg.float_mode, variant(h), h->stream));
-  if ((rc = apply_delay(h, sp.out, n, sp.out_stride_steps, false))) return rc;
+  if ((rc = apply_delay(h, sp.out, n, sp.out_stride_steps, false, sp.active))) return rc;
   h->steps += (uint64_t)n;
   return FS_OK;
 }
@@ -451,8 +458,6 @@ FS_API int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_
   if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
     return set_err(h, FS_E_INVALID, "fs_step_masked: p2 actions required for FS_P2_EXTERNAL");
   if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
-  if (h->cfg.frame_delay > 0)
-    return set_err(h, FS_E_UNSUPPORTED, "fs_step_masked: the delayed-frame queues advance in lockstep");
   return step_common(h, 1, p1_act, p2_act, flags, 0, nullptr, active);
 }
 

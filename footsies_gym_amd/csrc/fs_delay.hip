@@ -4,8 +4,9 @@
 // appends frame_delay copies of state(-1) (FE:493, 502-504); step() appends the new
 // state and pops the oldest, whose observation / info is returned while reward and
 // termination come from the new state (FE:532-535, 556-566).  Here every arena has a
-// ring of d packed records; all arenas step together, so global step s uses slot
-// s mod d: read the record written d steps ago, write this step's.  A row whose frame
+// ring of d packed records and a head slot: each of its steps reads the record written d of
+// its steps ago from the head slot, writes this step's there and advances the head (arenas
+// that fs_step_masked leaves idle keep theirs, like separate FootsiesEnvs).  A row whose frame
 // is -1 starts an episode (state(-1) is only emitted by a reset): the ring is refilled
 // with d copies and the row is left as is.  In same-step auto-reset a terminal row's
 // final_* outputs take the delayed record (the popped state) before the refill.
@@ -74,11 +75,12 @@ __global__ __launch_bounds__(256) void k_delay(DelayParams p) {
   if (a >= p.n_envs) return;
   const uint32_t N = (uint32_t)p.n_envs;
   const uint32_t row_step = (uint32_t)p.out_stride_steps * N;
+  if (p.active && !p.active[a]) return;  // an idle arena: no row, no shift
   auto slot_ptr = [&](uint32_t slot) { return p.ring + 2 * ((size_t)slot * N + (uint32_t)a); };
+  uint32_t slot = p.head[a];
   for (int t = 0; t < p.n_steps; t++) {
     const uint32_t r = (uint32_t)t * row_step + (uint32_t)a;
     const Rec cur = gather(p.out, r, false);
-    const uint32_t slot = (uint32_t)((p.step0 + (uint64_t)t) % (uint64_t)p.delay);
     if ((int32_t)cur.a.z == -1) {  // state(-1): the reset refills the queue
       if (!p.refill_only && p.same_step && p.out.terminated[r]) {
         const uint4* q = slot_ptr(slot);
@@ -96,7 +98,9 @@ __global__ __launch_bounds__(256) void k_delay(DelayParams p) {
       q[1] = cur.b;
       scatter(p.out, r, old, false);
     }
+    slot = slot + 1 == (uint32_t)p.delay ? 0u : slot + 1;  // (a refill leaves every slot equal)
   }
+  if (!p.refill_only) p.head[a] = (uint8_t)slot;
 }
 
 }  // namespace

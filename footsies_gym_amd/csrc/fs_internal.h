@@ -111,7 +111,8 @@ struct DelayParams {
   int delay;            // d
   int n_steps;          // rows to process (1 for fs_step / fs_reset)
   int out_stride_steps;
-  uint64_t step0;       // global step index of the first row
+  uint8_t* head;        // [N] per arena: the ring slot its next step reads and overwrites
+  const uint8_t* active;  // fs_step_masked: only these arenas stepped (nullptr = all)
   int refill_only;      // 1: after fs_reset / fs_create (no queue shift)
   int same_step;        // FS_AUTORESET_SAME_STEP: a terminal row's final_* take the delayed record
 };

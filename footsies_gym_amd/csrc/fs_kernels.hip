@@ -50,6 +50,16 @@ __shared__ Tables sT;
 
 constexpr int kBlock = 256;
 
+// Where a kernel reads the tables from: G = false, the LDS image every block stages (sT, sBot);
+// G = true, the __constant__ images in global memory through the vector L1 / L2 (kTables, kBot).
+// The fused launches stage (one copy serves hundreds of ticks); a one-tick launch (k_step) reads
+// them in place, which costs less than staging the image in every block for a single tick.
+template <bool G>
+__device__ __forceinline__ const Tables& tabs() {
+  if constexpr (G) return kTables;
+  else return sT;
+}
+
 // ---------------------------------------------------------------------------
 // packed fighter word (u64), one per fighter in DevState::fpk
 //   [0,5) action idx | [5,14) action frame | [14,19) hitstun | [19,21) vital |
@@ -263,7 +273,8 @@ __device__ __forceinline__ void set_action(Fighter& f, int a) {  // SetCurrentAc
 // ActionInfo (fs_tables.h) travels in registers as its raw 16 bytes: selecting
 // between two struct values (HIP's uint4 included) would go through scratch memory.
 typedef uint32_t AInfo __attribute__((ext_vector_type(4)));  // a native vector: selects stay in registers
-__device__ __forceinline__ AInfo action_info(int a) { return reinterpret_cast<const AInfo*>(sT.action)[a]; }
+template <bool G>
+__device__ __forceinline__ AInfo action_info(int a) { return reinterpret_cast<const AInfo*>(tabs<G>().action)[a]; }
 __device__ __forceinline__ AInfo stand_info() {  // action_info(A_STAND), as constants
   AInfo i;
   i.x = kStandInfo[0];
@@ -313,7 +324,8 @@ __device__ __forceinline__ ReqMasks req_masks(const Fighter& f, AInfo ai) {
 }
 
 typedef uint32_t RInfo __attribute__((ext_vector_type(4)));  // ReqInfo: take0, buffer0, rec0, pad
-__device__ __forceinline__ RInfo req_info(int a) { return reinterpret_cast<const RInfo*>(sT.req)[a]; }
+template <bool G>
+__device__ __forceinline__ RInfo req_info(int a) { return reinterpret_cast<const RInfo*>(tabs<G>().req)[a]; }
 
 // One RequestAction(a) of a chain; `took` / `rec` collect what SetCurrentAction did.
 __device__ __forceinline__ void request(Fighter& f, ReqMasks& m, bool& took, uint32_t& rec, int a, RInfo q,
@@ -331,12 +343,13 @@ __device__ __forceinline__ void request(Fighter& f, ReqMasks& m, bool& took, uin
 // UpdateActionRequest (F:201-286): hasWon's RequestAction(WIN), the reserved / buffered early
 // returns, then the request chain as one table read; branch-free apart from the hasWon skip.
 // Returns whether SetCurrentAction ran; then *rec is the new action's frame-0 record.
+template <bool G>
 __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEval& e, AInfo ai, uint32_t* rec) {
   ReqMasks m = req_masks(f, ai);
   bool took = false;
   uint32_t r = 0;
   if (f.won) {  // F:204-208 (hasWon is only set between KO and the next SetupBattleStart)
-    request(f, m, took, r, A_WIN, req_info(A_WIN), true);
+    request(f, m, took, r, A_WIN, req_info<G>(A_WIN), true);
     f.frame = took ? 0 : f.frame;
     f.hits = took ? 0 : f.hits;
     f.rsv = took ? NONE : f.rsv;
@@ -361,7 +374,7 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   // lanes that differ in action but not in inputs read different LDS banks)
   const uint32_t in8 = ((9u * cls + 3u * e.atk + e.dash) << 3) | (e.held << 1) | (uint32_t)f.prox;
   const uint32_t idx = ((uint32_t)f.act << 8) | (in8 ^ (uint32_t)f.act);
-  const uint32_t q = sT.req_table[early ? (uint32_t)(kReqEarly + a0) : idx];
+  const uint32_t q = tabs<G>().req_table[early ? (uint32_t)(kReqEarly + a0) : idx];
   const bool set = ((q >> 11) & 1u) != 0;  // SetCurrentAction ran (F:546-563)
   const bool bset = ((q >> 10) & 1u) != 0;
   f.act = set ? (int)(q & 31u) : f.act;
@@ -399,21 +412,24 @@ struct RecGeo {
   F4 hurt;  // hurtbox 0 (x offset, width / 2), hurtbox 1
   F4 hit;   // hitbox 0 (x offset, width / 2), hitbox 1
 };
+template <bool G>
 __device__ __forceinline__ RecGeo frame_rec(uint32_t k, uint32_t rec) {
-  const uint32_t off = __umul24(k, (uint32_t)sizeof(sT.rec_push[0])) + __umul24(rec, 16u);
+  const Tables& T = tabs<G>();
+  const uint32_t off = __umul24(k, (uint32_t)sizeof(T.rec_push[0])) + __umul24(rec, 16u);
   auto at = [&](const void* base) {
     return *reinterpret_cast<const F4*>(reinterpret_cast<const char*>(base) + off);
   };
   RecGeo g;
-  g.push = at(&sT.rec_push[0][0]);
-  g.hurt = at(&sT.rec_hurt[0][0]);
-  g.hit = at(&sT.rec_hit[0][0]);
+  g.push = at(&T.rec_push[0][0]);
+  g.hurt = at(&T.rec_hurt[0][0]);
+  g.hit = at(&T.rec_hit[0][0]);
   return g;
 }
 
 // the frame record of (act, frame)
+template <bool G>
 __device__ __forceinline__ int frame_record(const Fighter& f) {
-  return sT.rec_index[f.act * kFrameStride + min(f.frame, kFrameStride - 1)];
+  return tabs<G>().rec_index[f.act * kFrameStride + min(f.frame, kFrameStride - 1)];
 }
 
 // UpdateBoxes (F:671-697): world x of every box of the record, `R` being the record in
@@ -626,6 +642,11 @@ static_assert(move_plan_len(MP_FAR1) <= 8 * 16 && attack_plan_len(AP_DELAY_SPECI
               "plans fit eight code words");
 __constant__ const BotTables kBot = make_bot_tables();
 __shared__ BotTables sBot;
+template <bool G>
+__device__ __forceinline__ const BotTables& bots() {
+  if constexpr (G) return kBot;
+  else return sBot;
+}
 
 // Copy the kTables image (fs_tables.h) and the bot tables into LDS: every thread issues all
 // of its loads before any store, so the block waits for one round trip, not one per table.
@@ -691,6 +712,7 @@ __device__ __forceinline__ float bot_distance(float x1, float x2) {
 // q = this lane's queue (0 = attack on the P1 lane, 1 = movement on the P2 lane).  Both lanes of
 // the pair must call it (it exchanges with the partner); it returns the bot's input on both.
 __device__ __forceinline__ uint32_t xpair(uint32_t v);
+template <bool G>
 __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dist, uint32_t opp_act) {
   const float d = b.prev_dist;
   const uint32_t opp = b.prev_opp;
@@ -699,7 +721,7 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dis
   const uint32_t bucket = d > 4.0f ? 0u : d > 3.0f ? 1u : d > 2.5f ? 2u : d > 2.0f ? 3u : 4u;
   const bool busy = b.plan != 0;
   const uint32_t p = busy ? b.plan - 1 : 0u, i = b.idx;
-  const uint32_t code = (sBot.codes[q][p][i >> 4] >> (2 * (i & 15))) & 3u;
+  const uint32_t code = (bots<G>().codes[q][p][i >> 4] >> (2 * (i & 15))) & 3u;
   const uint32_t mine = busy ? (q ? code : code << 2) : 0u;  // Left / Right bits, or IN_ATTACK
   const bool o_busy = xpair((uint32_t)busy) != 0;
   const bool mbusy = q ? busy : o_busy, abusy = q ? o_busy : busy;
@@ -711,11 +733,11 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dis
   const uint32_t x2 = rng_next(s2);
   const uint4 s0 = b.rng;
   b.rng = (dm & da) ? s2 : (dm | da) ? s1 : s0;
-  const BotDraw w = sBot.draw[q][bucket];
+  const BotDraw w = bots<G>().draw[q][bucket];
   const uint32_t drawn = (w.map >> (4 * draw_mod((!q & dm) ? x2 : x1, w))) & 15u;
   const uint32_t newp = (!q & forced) ? (uint32_t)AP_TWO_HIT : drawn;
   const uint32_t i1 = i + 1;
-  b.plan = busy ? (i1 == sBot.len[q][p] ? 0u : b.plan) : newp + 1;
+  b.plan = busy ? (i1 == bots<G>().len[q][p] ? 0u : b.plan) : newp + 1;
   b.idx = busy ? i1 : 0u;
   return mine | xpair(mine);
 }
@@ -753,6 +775,7 @@ __device__ __forceinline__ uint2 pack_bot(const FullBot& b, uint32_t input) {
 // previous call's state decides; a bot whose fightStates[5] is still null (never Reset, first
 // call) answers 0 without touching its queues or the RNG.  P1's forward is Right (AI:380-388),
 // so its movement codes are mirrored.
+template <bool G>
 __device__ __forceinline__ uint32_t bot_full_next(FullBot& b, uint4& rng, uint32_t k, float dist, uint32_t opp_act) {
   const bool ready = b.ready;
   const float d = b.prev_dist;
@@ -765,25 +788,25 @@ __device__ __forceinline__ uint32_t bot_full_next(FullBot& b, uint4& rng, uint32
   uint32_t in = 0;
   if (b.mplan != 0) {  // moveQueue.Dequeue
     const uint32_t p = b.mplan - 1, i = b.midx;
-    const uint32_t c = (sBot.codes[1][p][i >> 4] >> (2 * (i & 15))) & 3u;
+    const uint32_t c = (bots<G>().codes[1][p][i >> 4] >> (2 * (i & 15))) & 3u;
     in |= k == 0 ? (((c & 1u) << 1) | (c >> 1)) : c;
     b.midx = i + 1;
-    if (b.midx == sBot.len[1][p]) b.mplan = 0;
+    if (b.midx == bots<G>().len[1][p]) b.mplan = 0;
   } else {  // SelectMovement (AI:68-126)
-    const BotDraw w = sBot.draw[1][bucket];
+    const BotDraw w = bots<G>().draw[1][bucket];
     b.mplan = ((w.map >> (4 * draw_mod(rng_next(rng), w))) & 15u) + 1;
     b.midx = 0;
   }
   if (b.aplan != 0) {  // attackQueue.Dequeue
     const uint32_t p = b.aplan - 1, i = b.aidx;
-    in |= ((sBot.codes[0][p][i >> 4] >> (2 * (i & 15))) & 1u) << 2;
+    in |= ((bots<G>().codes[0][p][i >> 4] >> (2 * (i & 15))) & 1u) << 2;
     b.aidx = i + 1;
-    if (b.aidx == sBot.len[0][p]) b.aplan = 0;
+    if (b.aidx == bots<G>().len[0][p]) b.aplan = 0;
   } else if (attack_forced(bucket, opp)) {  // SelectAttack without a draw (AI:130-133, 147-151)
     b.aplan = AP_TWO_HIT + 1;
     b.aidx = 0;
   } else {  // SelectAttack (AI:128-190)
-    const BotDraw w = sBot.draw[0][bucket];
+    const BotDraw w = bots<G>().draw[0][bucket];
     b.aplan = ((w.map >> (4 * draw_mod(rng_next(rng), w))) & 15u) + 1;
     b.aidx = 0;
   }
@@ -1080,16 +1103,17 @@ __device__ __forceinline__ uint4 xpair4(uint4 v) {
   o.w = xpair(v.w);
   return o;
 }
+template <bool G>
 __device__ __forceinline__ void actors_request(Lane& L, const Actors& ac, float dist, uint32_t p1_act,
                                                uint32_t p2_act) {
   uint4 r = L.rng;
   if (ac.p1_bot) {
-    if (L.k == 0) L.bin = bot_full_next(L.fb, r, 0, dist, p2_act);
+    if (L.k == 0) L.bin = bot_full_next<G>(L.fb, r, 0, dist, p2_act);
     const uint4 o = xpair4(r);
     r = L.k == 1 ? o : r;
   }
   if (L.p2bot) {
-    if (L.k == 1) L.bin = bot_full_next(L.fb, r, 1, dist, p1_act);
+    if (L.k == 1) L.bin = bot_full_next<G>(L.fb, r, 1, dist, p1_act);
     const uint4 o = xpair4(r);
     r = L.k == 0 ? o : r;
   }
@@ -1108,7 +1132,7 @@ __device__ __forceinline__ void actors_request(Lane& L, const Actors& ac, float 
 //   pushboxes at x = -2 / +2 neither overlap nor touch the stage edges).
 //   Fight: frameCount = -1, recording index 0, state(-1) emitted, and the bots'
 //   first RequestNextInput.
-template <int FM, int V>
+template <int FM, int V, bool G = false>
 __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko, const Actors& ac) {
   constexpr bool BOT = V == FS_P2_BOT;
   if (after_ko) {
@@ -1142,10 +1166,10 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko, const Actors
   L.frame_count = -1;
   L.rec_count = 0;
   if constexpr (BOT) {
-    const uint32_t bi = bot_next_input(L.bot, L.k, bot_distance<FM>(x1, x2), p1_act);
+    const uint32_t bi = bot_next_input<G>(L.bot, L.k, bot_distance<FM>(x1, x2), p1_act);
     L.bin = L.k == 1 ? bi : L.bin;
   } else if constexpr (V == kActors) {
-    actors_request(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
+    actors_request<G>(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
   }
 }
 
@@ -1234,14 +1258,14 @@ __device__ __forceinline__ void settle_w(uint32_t& next) {
   }
 }
 
-template <int FM, int P2, int WAIT = -1>
+template <int FM, int P2, int WAIT = -1, bool G = false>
 __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   const DevOutputs& o = p.out;
   const uint32_t k = L.k;
   const Actors ac{p.p1_bot != 0, p.p2_resets != 0, p.p2_noop != 0};
   if (L.pending) {  // FS_AUTORESET_NEXT_STEP: this step runs the reset burst only
-    reset_burst<FM, P2>(L, true, ac);
+    reset_burst<FM, P2, G>(L, true, ac);
     L.pending = false;
     L.has_term = false;
     L.cum = 0.0;
@@ -1276,20 +1300,20 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   increment_action_frame(L.f, ai);
   // the record if the action continues, read alongside the request's ReqInfo reads; a
   // request that sets an action returns that action's frame-0 record
-  const int rec_cont = frame_record(L.f);
+  const int rec_cont = frame_record<G>(L.f);
   uint32_t rec_set;
-  const bool set = update_action_request(L.f, e, ai, &rec_set);
+  const bool set = update_action_request<G>(L.f, e, ai, &rec_set);
   L.f.rec = set ? (int)rec_set : rec_cont;
   // One LDS round trip for everything the rest of the tick reads from the tables: my frame
   // record, the y half of the box-pair overlaps (records only, kTables.ybits) and the hit
   // resolution of the partner's record at its hit count (the record index and the hit count
   // cross the pair first).
-  const RecGeo R = frame_rec(k, (uint32_t)L.f.rec);
+  const RecGeo R = frame_rec<G>(k, (uint32_t)L.f.rec);
   const uint32_t o_rec = (uint32_t)xpair(L.f.rec);
   const uint32_t o_hits = (uint32_t)xpair(L.f.hits);
   static_assert(kNumFrameRecs <= 64, "ybits rows are 64 records wide");
-  const uint32_t ym = sT.ybits[(o_rec << 6) | (uint32_t)L.f.rec];
-  const U4 res = reinterpret_cast<const U4*>(sT.resolve)[(o_rec << 2) | o_hits];
+  const uint32_t ym = tabs<G>().ybits[(o_rec << 6) | (uint32_t)L.f.rec];
+  const U4 res = reinterpret_cast<const U4*>(tabs<G>().resolve)[(o_rec << 2) | o_hits];
   update_movement<FM>(L.f, R.push.z);
   update_boxes<FM>(L.f, R);
   // the partner's hitbox half-widths (its own record's)
@@ -1304,7 +1328,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   hitbox_hurtbox_collision<FM>(L.f, k, R.hurt, o_hw0, o_hw1, res, ym);
   // the next tick's ActionInfo, issued now so its LDS latency hides behind the KO test, the
   // reward and the stores (only the reset paths below change the action again: to STAND)
-  const AInfo ai_next = action_info(L.f.act);
+  const AInfo ai_next = action_info<G>(L.f.act);
   // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes: each
   // lane's flags (bit 0: vital 0, bit 1: guard dropped this tick; both fields are 0..3) cross
   // the pair once, then fl1 / fl2 are P1's / P2's
@@ -1333,7 +1357,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.f.hold = 0;
     if (p.autoreset_mode == FS_AUTORESET_SAME_STEP) {
       write_final(L, o, r);
-      reset_burst<FM, P2>(L, true, ac);
+      reset_burst<FM, P2, G>(L, true, ac);
       L.cum = 0.0;
       L.has_term = false;
     } else {
@@ -1346,14 +1370,14 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
       const uint32_t o_act = xpair((uint32_t)L.f.act);
       const float x1 = k == 0 ? L.f.x : o_x, x2 = k == 0 ? o_x : L.f.x;
       const uint32_t p1_act = k == 0 ? (uint32_t)L.f.act : o_act;
-      const uint32_t bi = bot_next_input(L.bot, k, bot_distance<FM>(x1, x2), p1_act);
+      const uint32_t bi = bot_next_input<G>(L.bot, k, bot_distance<FM>(x1, x2), p1_act);
       L.bin = k == 1 ? bi : L.bin;
     } else if constexpr (P2 == kActors) {  // the same, for the per-arena actors
       const float o_x = xpair(L.f.x);
       const uint32_t o_act = xpair((uint32_t)L.f.act);
       const float x1 = k == 0 ? L.f.x : o_x, x2 = k == 0 ? o_x : L.f.x;
       const uint32_t p1_act = k == 0 ? (uint32_t)L.f.act : o_act, p2_act = k == 1 ? (uint32_t)L.f.act : o_act;
-      actors_request(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
+      actors_request<G>(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
     }
     L.has_term = false;
   }
@@ -1411,7 +1435,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   if constexpr (FUSED && !HASH && !POL) next = row_load((reads ? src : p.p1) + (uint32_t)a);
   else next = fetch(0);
   if constexpr (POL) stage_policy(p.pol);
-  stage_tables();
+  if constexpr (FUSED) stage_tables();
   if constexpr (POL) {
     if ((l & ~63) >= 2 * p.n_envs) return;  // the whole wave is past the last arena
   } else {
@@ -1420,7 +1444,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   if constexpr (!FUSED) {
     if (p.active && !p.active[a]) return;  // fs_step_masked: this arena does not tick
   }
-  L.ai = action_info(L.f.act);
+  L.ai = action_info<!FUSED>(L.f.act);
   if constexpr (POL) {
     const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
     const uint32_t arena0 = (uint32_t)(l & ~63) >> 1;
@@ -1483,7 +1507,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     }
   } else {
     uint32_t none = 0;
-    env_step<FM, P2>(L, next & 7u, p, (uint32_t)a, none);
+    env_step<FM, P2, -1, true>(L, next & 7u, p, (uint32_t)a, none);
   }
   if (active) store_lane<P2>(L, p.st, a);
 }

@@ -84,13 +84,22 @@ class FootsiesSim:
         check(lib().fs_create(C.byref(cfg), C.byref(h)), None)
         self._h = h
         self.cfg = cfg
-        # outputs: torch tensors bound into the library
+        # outputs: torch tensors bound into the library, all views of one device buffer (256-B
+        # aligned slices) so that the host side fetches a step's outputs with one copy
         n = self.num_envs
         self._out = {}
+        layout, total = [], 0
+        for name, (dt, cols) in _abi.OUTPUT_SPEC.items():
+            shape = (n, cols) if cols > 1 else (n,)
+            nbytes = n * cols * np.dtype(dt).itemsize
+            layout.append((name, dt, shape, total, nbytes))
+            total += (nbytes + 255) // 256 * 256
         with torch.cuda.device(self.device):
-            for name, (dt, cols) in _abi.OUTPUT_SPEC.items():
-                shape = (n, cols) if cols > 1 else (n,)
-                self._out[name] = torch.zeros(shape, dtype=getattr(torch, _TORCH_DTYPES[dt]), device=self.device)
+            self._out_buf = torch.zeros(total, dtype=torch.uint8, device=self.device)
+        for name, dt, shape, off, nbytes in layout:
+            self._out[name] = self._out_buf[off:off + nbytes].view(getattr(torch, _TORCH_DTYPES[dt])).view(shape)
+        self._out_layout = layout
+        self._host_buf = None  # pinned mirror of _out_buf, allocated on first use
         # the library's creation-time outputs (state(-1)) into the bound buffers
         own = _abi.fs_outputs()
         check(lib().fs_outputs_get(h, C.byref(own)), h)
@@ -209,9 +218,19 @@ class FootsiesSim:
         check(lib().fs_pack_outputs(self._h, C.c_void_p(dst.data_ptr())), self._h)
         return dst
 
-    def outputs_numpy(self):
-        _torch().cuda.synchronize(self.device)
-        return {k: v.cpu().numpy() for k, v in self._out.items()}
+    def outputs_numpy(self, copy=True):
+        """The current outputs on the host, fetched with one device-to-host copy into a pinned
+        buffer.  copy=False returns views of that buffer, overwritten by the next call."""
+        torch = _torch()
+        if self._host_buf is None:
+            self._host_buf = torch.empty(self._out_buf.numel(), dtype=torch.uint8, pin_memory=True)
+            self._host_np = self._host_buf.numpy()
+        self._host_buf.copy_(self._out_buf)  # ordered after the library's work on this stream
+        out = {}
+        for name, dt, shape, off, nbytes in self._out_layout:
+            v = self._host_np[off:off + nbytes].view(dt).reshape(shape)
+            out[name] = v.copy() if copy else v
+        return out
 
     def env_state(self):
         arr = (_abi.fs_env_state * self.num_envs)()

@@ -19,23 +19,27 @@ from . import _abi, battle_state
 from . import spaces as sp
 from .simulator import FootsiesSim, decode_actions, encode_actions
 
+try:  # pragma: no cover - depends on the environment
+    from gymnasium.vector import VectorEnv as _VectorEnvBase  # a gymnasium.vector.VectorEnv when importable
+except Exception:  # gymnasium is not installed in this image
+    _VectorEnvBase = object
+
 
 def obs_info_from_outputs(out, prefix=""):
     """Host-side view of one set of kernel outputs -> (obs, info) batches with the
     reference dtypes: MultiDiscrete -> int64, Box -> float32 (FE:157-168, 336-380)."""
-    g = out[prefix + "guard"]
-    obs = {
-        "guard": np.asarray(g, dtype=np.int64),
-        "move": np.asarray(out[prefix + "move"], dtype=np.int64),
-        "move_frame": np.asarray(out[prefix + "move_frame"], dtype=np.float32),
-        "position": np.asarray(out[prefix + "position"], dtype=np.float32),
+    obs = {  # (always new arrays: ``out`` may be views of a reused host buffer)
+        "guard": np.array(out[prefix + "guard"], dtype=np.int64),
+        "move": np.array(out[prefix + "move"], dtype=np.int64),
+        "move_frame": np.array(out[prefix + "move_frame"], dtype=np.float32),
+        "position": np.array(out[prefix + "position"], dtype=np.float32),
     }
-    act = np.asarray(out[prefix + "action"])
+    act = decode_actions(out[prefix + "action"])  # (N, 2, 3): both players in one pass
     hs = np.asarray(out[prefix + "hitstun"], dtype=np.int64)
     info = {
         "frame": np.asarray(out[prefix + "frame"], dtype=np.int64),
-        "p1_action": decode_actions(act[:, 0]),
-        "p2_action": decode_actions(act[:, 1]),
+        "p1_action": act[:, 0],
+        "p2_action": act[:, 1],
         "p1_hitstun": hs[:, 0],
         "p2_hitstun": hs[:, 1],
     }
@@ -46,17 +50,19 @@ def obs_info_from_outputs(out, prefix=""):
 def step_result_from_outputs(out, autoreset_mode="same_step"):
     """(obs, rewards, terminations, truncations, infos) from host copies of the outputs."""
     obs, info = obs_info_from_outputs(out)
-    rewards = np.asarray(out["reward"], dtype=np.float64)
+    rewards = np.array(out["reward"], dtype=np.float64)
     term = np.asarray(out["terminated"]).astype(bool)
     trunc = np.asarray(out["truncated"]).astype(bool)
     if autoreset_mode == "same_step" and term.any():
-        fobs, finfo = obs_info_from_outputs(out, prefix="final_")
         idx = np.nonzero(term)[0]
+        # only the terminated arenas' final outputs are converted
+        fobs, finfo = obs_info_from_outputs({k: v[idx] for k, v in out.items() if k.startswith("final_")},
+                                            prefix="final_")
         final_obs = np.empty(len(term), dtype=object)
         final_info = np.empty(len(term), dtype=object)
-        for i in idx:
-            final_obs[i] = {k: v[i] for k, v in fobs.items()}
-            final_info[i] = {k: v[i] for k, v in finfo.items()}
+        # per-arena dicts built from row iterators (one pass per key, not one index per entry)
+        final_obs[idx] = [dict(zip(fobs, vals)) for vals in zip(*(iter(v) for v in fobs.values()))]
+        final_info[idx] = [dict(zip(finfo, vals)) for vals in zip(*(iter(v) for v in finfo.values()))]
         info["final_observation"] = final_obs
         info["_final_observation"] = term.copy()
         info["final_info"] = final_info
@@ -64,8 +70,10 @@ def step_result_from_outputs(out, autoreset_mode="same_step"):
     return obs, rewards, term, trunc, info
 
 
-class FootsiesVectorEnv:
-    """N FOOTSIES arenas as one vector environment.
+class FootsiesVectorEnv(_VectorEnvBase):
+    """N FOOTSIES arenas as one vector environment (a ``gymnasium.vector.VectorEnv`` subclass
+    whenever gymnasium is importable; its reset / step / close are overridden here, so neither
+    0.29's async hooks nor 1.x's base methods are used).
 
     Parameters follow FootsiesEnv.__init__ (FE:34-53) where they still have a
     meaning: ``frame_delay`` (observations and info ``frame_delay`` steps old, FE:126-131,
@@ -81,6 +89,9 @@ class FootsiesVectorEnv:
     """
 
     metadata = {"render_modes": [], "render_fps": 60}
+    render_mode = None
+    spec = None
+    is_vector_env = True
 
     def __init__(self, num_envs, device=0, opponent=None, dense_reward=True, frame_delay=0,
                  autoreset_mode="same_step", float_mode="strict", seed=0, vs_player=False, by_example=False,
@@ -109,6 +120,7 @@ class FootsiesVectorEnv:
         self.observation_space = sp.batch_observation_space(self.num_envs)
         self.action_space = sp.batch_action_space(self.num_envs)
         self.reward_range = (-1, 1)
+        self.closed = False
         self._last = None  # most recent (obs, info) for the opponent callable
 
     # -- gymnasium.vector.VectorEnv API ---------------------------------------------------
@@ -125,7 +137,7 @@ class FootsiesVectorEnv:
         if self.output == "torch":
             self._last = (out, None)
             return {k: out[k] for k in ("guard", "move", "move_frame", "position")}, out
-        obs, info = obs_info_from_outputs(self.sim.outputs_numpy())
+        obs, info = obs_info_from_outputs(self.sim.outputs_numpy(copy=False))
         self._last = (obs, info)
         return obs, info
 
@@ -170,7 +182,7 @@ class FootsiesVectorEnv:
             obs = {k: out[k] for k in ("guard", "move", "move_frame", "position")}
             self._last = (obs, out)
             return obs, out["reward"], out["terminated"], out["truncated"], out
-        obs, rew, term, trunc, info = step_result_from_outputs(self.sim.outputs_numpy(), self.autoreset_mode)
+        obs, rew, term, trunc, info = step_result_from_outputs(self.sim.outputs_numpy(copy=False), self.autoreset_mode)
         self._last = (obs, info)
         return obs, rew, term, trunc, info
 
@@ -196,8 +208,11 @@ class FootsiesVectorEnv:
         self._last = (obs, info)
         return obs, rew, term, trunc, info
 
-    def close(self):
-        self.sim.close()
+    def close(self, **kwargs):
+        sim = getattr(self, "sim", None)  # (also from a base-class __del__ after a failed __init__)
+        if sim is not None and not getattr(self, "closed", False):
+            sim.close()
+        self.closed = True
 
     # -- FootsiesEnv extras (FE:432-480) ------------------------------------------------
     def save_battle_state(self):

@@ -235,7 +235,8 @@ int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags
  * and their outputs (which then still hold their previous step's values).  This
  * lets arenas advance at their own pace, as N separate FootsiesEnv instances do
  * under a frame-skipping wrapper (wrappers/frame_skip.py:63-80).  active lives
- * where flags says the actions do.  FS_E_UNSUPPORTED with frame_delay > 0. */
+ * where flags says the actions do.  With frame_delay > 0 each arena's delayed-frame
+ * queue advances with that arena's own steps (every FootsiesEnv keeps its own deque). */
 int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, const uint8_t* active, int flags);
 
 /* n Fight ticks in one kernel launch (fused rollout).  Actions: device arrays

@@ -1234,9 +1234,8 @@ OR_EXPORT int or_step(or_handle C, const uint8_t* p1, const uint8_t* p2) {
 OR_EXPORT int or_step_masked(or_handle C, const uint8_t* p1, const uint8_t* p2, const uint8_t* active) {
   if (!C || (!p1 && C->cfg.p1_mode != FS_P1_BOT) || !active) return FS_E_INVALID;
   if (C->cfg.p2_mode == FS_P2_EXTERNAL && !p2) return FS_E_INVALID;
-  if (C->cfg.frame_delay > 0) return FS_E_UNSUPPORTED;
 #pragma omp parallel for schedule(static) if (C->n >= 1024)
-  for (int i = 0; i < C->n; i++)
+  for (int i = 0; i < C->n; i++)  /* (each arena's delayed-frame queue advances with its own steps) */
     if (active[i]) fe_step_arena(C, i, p1 ? p1[i] : 0, p2 ? p2[i] : 0);
   C->steps++;
   return FS_OK;

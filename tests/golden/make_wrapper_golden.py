@@ -39,8 +39,8 @@ from tests.golden.make_golden import state_json  # noqa: E402
 class GameEnv(FootsiesEnv):
     """The reference FootsiesEnv whose game is a private one-arena oracle."""
 
-    def __init__(self, seed, dense_reward):
-        super().__init__(skip_instancing=True, dense_reward=dense_reward)
+    def __init__(self, seed, dense_reward, frame_delay=0):
+        super().__init__(skip_instancing=True, dense_reward=dense_reward, frame_delay=frame_delay)
         self.game = binding.Oracle(1, p2_mode=_abi.FS_P2_BOT, dense_reward=dense_reward,
                                    autoreset_mode=_abi.FS_AUTORESET_NEXT_STEP, base_seed=seed)
         self._p1 = None
@@ -72,9 +72,9 @@ def as_tuple(a):
     return ((a & 1) != 0, (a & 2) != 0, (a & 4) != 0)
 
 
-def run(name, stack, n, steps, seed, sticky, dense, discrete):
+def run(name, stack, n, steps, seed, sticky, dense, discrete, frame_delay=0):
     rng = np.random.default_rng(seed + 7)
-    bases = [GameEnv(seed + i, dense) for i in range(n)]
+    bases = [GameEnv(seed + i, dense, frame_delay) for i in range(n)]
     envs = [stack(b) for b in bases]
     rec = {"guard": [], "move": [], "move_frame": [], "position": []}
     acts = np.zeros((steps, n), np.uint8)
@@ -103,6 +103,8 @@ def run(name, stack, n, steps, seed, sticky, dense, discrete):
             rec[k].append([np.asarray(o[k], dtype=np.float64).reshape(-1) for o in row])
     out = {"%s/actions" % name: acts, "%s/reward" % name: rew, "%s/terminated" % name: term,
            "%s/is_reset" % name: is_reset, "%s/config" % name: np.array([n, steps, seed, int(dense)], np.int64)}
+    if frame_delay:
+        out["%s/frame_delay" % name] = np.array(frame_delay, np.int64)
     for k in rec:
         out["%s/%s" % (name, k)] = np.array(rec[k])
         out["%s/first/%s" % (name, k)] = np.array([np.asarray(o[k], np.float64).reshape(-1) for o in first])
@@ -125,6 +127,9 @@ def main():
     data.update(run("skip_raw", lambda b: FootsiesFrameSkipped(b), 12, 700, 30, 0.5, False, False))
     data.update(run("norm_noguard", lambda b: FootsiesNormalized(b, normalize_guard=False), 8, 500, 40, 0.5, True,
                     False))
+    # frame skipping over FootsiesEnv's delayed-frame queue (FE:126-131, 532-535): every env's
+    # queue advances with its own steps
+    data.update(run("skip_delay", lambda b: FootsiesFrameSkipped(b), 12, 700, 60, 0.6, True, False, frame_delay=3))
     data.update(run("stats_disc", lambda b: FootsiesStatistics(FootsiesActionCombinationsDiscretized(b)), 16, 4000,
                     50, 0.97, True, True))
     np.savez_compressed(os.path.join(HERE, "wrapper_golden.npz"), **data)

@@ -12,11 +12,11 @@ AR = {"same_step": _abi.FS_AUTORESET_SAME_STEP, "next_step": _abi.FS_AUTORESET_N
 
 
 class OracleVectorEnv:
-    def __init__(self, num_envs, oracle_lib, dense_reward=True, seed=0, autoreset_mode="next_step"):
+    def __init__(self, num_envs, oracle_lib, dense_reward=True, seed=0, autoreset_mode="next_step", frame_delay=0):
         self.num_envs = num_envs
         self.autoreset_mode = autoreset_mode
         self.ora = oracle_lib.Oracle(num_envs, p2_mode=_abi.FS_P2_BOT, dense_reward=dense_reward,
-                                     autoreset_mode=AR[autoreset_mode], base_seed=seed)
+                                     autoreset_mode=AR[autoreset_mode], base_seed=seed, frame_delay=frame_delay)
         self.single_observation_space = sp.single_observation_space()
         self.single_action_space = sp.single_action_space()
 

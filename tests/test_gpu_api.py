@@ -113,8 +113,8 @@ def test_step_masked_matches_oracle(oracle_lib, p2):
 @pytest.mark.parametrize("name", wr.CASES)
 def test_wrappers_match_reference_gpu(name):
     from footsies_gym_amd.vector_env import FootsiesVectorEnv
-    wr.replay(name, lambda n, dense, seed: FootsiesVectorEnv(n, opponent=None, dense_reward=dense, seed=seed,
-                                                             autoreset_mode="next_step"))
+    wr.replay(name, lambda n, dense, seed, delay: FootsiesVectorEnv(n, opponent=None, dense_reward=dense, seed=seed,
+                                                                    autoreset_mode="next_step", frame_delay=delay))
 
 
 def test_battle_state_json_into_gpu_continues_like_oracle(oracle_lib):

@@ -76,3 +76,45 @@ def test_same_step_final_observation():
     assert info["final_info"][1]["frame"] == out["final_frame"][1]
     _, _, _, _, info2 = step_result_from_outputs(out, "next_step")
     assert "final_observation" not in info2
+
+
+def test_step_results_own_their_arrays():
+    """VectorEnv.step converts views of a reused pinned host buffer (outputs_numpy(copy=False)):
+    nothing it returns may alias that buffer."""
+    out = fake_outputs(5, term_rows=(2,))
+    obs, rew, term, trunc, info = step_result_from_outputs(out, "same_step")
+    before = {k: v.copy() for k, v in obs.items()}, rew.copy(), info["final_observation"][2]["position"].copy()
+    for v in out.values():
+        v[...] = 0
+    assert all(np.array_equal(obs[k], before[0][k]) for k in obs)
+    assert np.array_equal(rew, before[1]) and np.array_equal(info["final_observation"][2]["position"], before[2])
+
+
+def test_vector_env_subclasses_gymnasium_vector_env_when_importable(monkeypatch):
+    """With gymnasium importable, FootsiesVectorEnv is a gymnasium.vector.VectorEnv (a stand-in
+    module here: gymnasium is not installed in this image) and keeps its own reset/step/close."""
+    import importlib
+    import sys
+    import types
+    gym = types.ModuleType("gymnasium")
+    vec = types.ModuleType("gymnasium.vector")
+
+    class VectorEnv:
+        def step(self, actions):
+            raise AssertionError("base step called")
+
+    vec.VectorEnv = VectorEnv
+    gym.vector = vec
+    monkeypatch.setitem(sys.modules, "gymnasium", gym)
+    monkeypatch.setitem(sys.modules, "gymnasium.vector", vec)
+    import footsies_gym_amd.vector_env as ve
+    try:
+        mod = importlib.reload(ve)
+        assert issubclass(mod.FootsiesVectorEnv, VectorEnv)
+        for name in ("reset", "step", "close"):
+            assert getattr(mod.FootsiesVectorEnv, name) is not getattr(VectorEnv, name, None)
+        mod.FootsiesVectorEnv.close(object.__new__(mod.FootsiesVectorEnv))  # no sim yet: a no-op
+    finally:
+        monkeypatch.undo()
+        importlib.reload(ve)
+    assert ve.FootsiesVectorEnv.__mro__[1] is object

@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -68,3 +70,19 @@ def test_move_table_matches_reference_python():
     assert [(m[0], m[1], m[2]) for m in g["moves"]] == list(_abi.MOVES)
     acts = {a["id"]: a["frame_count"] for a in load()["actions"]}
     assert all(acts[mid] == dur for _, mid, dur in _abi.MOVES)  # durations == asset frameCount
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/Assets/Fighter/F00"),
+                    reason="the reference assets exist only in the build container")
+def test_f00_json_re_extracts_identically_from_the_reference_assets(tmp_path):
+    """data/f00.json is what tools/extract_f00.py reads out of the reference's Unity assets
+    (F00.asset, F00_AttackDataContainer.asset, Actions/*.asset, BattleScene.unity,
+    TimeManager.asset): a fresh extraction is byte-identical to the committed file."""
+    import subprocess
+    import sys
+    out = tmp_path / "f00.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "extract_f00.py"), str(out)],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, FOOTSIES_REF="/root/reference"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out.read_bytes() == open(os.path.join(ROOT, "data", "f00.json"), "rb").read()

@@ -11,7 +11,8 @@ from tests.oracle_vector_env import OracleVectorEnv
 
 @pytest.mark.parametrize("name", wr.CASES)
 def test_wrappers_match_reference_on_oracle(oracle_lib, name):
-    wr.replay(name, lambda n, dense, seed: OracleVectorEnv(n, oracle_lib, dense_reward=dense, seed=seed))
+    wr.replay(name, lambda n, dense, seed, delay: OracleVectorEnv(n, oracle_lib, dense_reward=dense, seed=seed,
+                                                                  frame_delay=delay))
 
 
 def test_discretized_action_bits():

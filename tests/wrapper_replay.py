@@ -7,12 +7,13 @@ import numpy as np
 from footsies_gym_amd import wrappers as W
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CASES = ("skip_norm", "skip_raw", "norm_noguard", "stats_disc")
+CASES = ("skip_norm", "skip_raw", "norm_noguard", "stats_disc", "skip_delay")
 STACKS = {
     "skip_norm": lambda b: W.FootsiesFrameSkipped(W.FootsiesNormalized(b, exact=True)),
     "skip_raw": lambda b: W.FootsiesFrameSkipped(b),
     "norm_noguard": lambda b: W.FootsiesNormalized(b, normalize_guard=False, exact=True),
     "stats_disc": lambda b: W.FootsiesStatistics(W.FootsiesActionCombinationsDiscretized(b)),
+    "skip_delay": lambda b: W.FootsiesFrameSkipped(b),
 }
 _CACHE = {}
 
@@ -36,10 +37,12 @@ def _check_obs(name, obs, exp, t):
 
 
 def replay(name, make_base):
-    """make_base(n, dense, seed) -> a next_step-autoreset vector env with the bot as P2."""
+    """make_base(n, dense, seed, frame_delay) -> a next_step-autoreset vector env with the bot
+    as P2."""
     z = load()
     n, steps, seed, dense = (int(v) for v in z[name + "/config"])
-    env = STACKS[name](make_base(n, bool(dense), seed))
+    delay = int(z.get(name + "/frame_delay", 0))
+    env = STACKS[name](make_base(n, bool(dense), seed, delay))
     obs, _ = env.reset()
     _check_obs(name, obs, lambda k: z["%s/first/%s" % (name, k)], -1)
     acts = z[name + "/actions"]
