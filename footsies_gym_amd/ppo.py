@@ -10,8 +10,12 @@ One iteration:
    same-step auto-reset that is the fresh round's state, so a terminal tick's successor is
    never bootstrapped through: done masks it).
 3. `epochs` x `minibatches` clipped-surrogate updates of the actor and critic (fp32 torch).
-   The old log-probabilities are recomputed in fp32 from the same network, so the first
-   ratio is exactly 1.
+   The importance ratio's old log-probabilities are the behaviour policy's: the log-probs the
+   bf16 kernel actor sampled with (`old_logp="behaviour"`, the default), or the same network
+   recomputed in fp32 (`old_logp="fp32"`, first ratio exactly 1).  Either way the iteration
+   reports how far the two are apart: `kl_behaviour_fp32`, the sample estimate
+   E_a~behaviour[log p_bf16(a) - log p_fp32(a)] of KL(bf16 actor || fp32 actor), and
+   `logp_abs_diff`, the mean |log p_bf16(a) - log p_fp32(a)|.
 4. The new actor weights are copied into the rollout's device buffers (no reallocation).
 
 Nothing leaves the GPU inside an iteration, and the simulator never waits on the host.
@@ -114,8 +118,11 @@ class PPOTrainer:
     rollout, all arenas in every minibatch round."""
 
     def __init__(self, sim, actor=None, critic=None, horizon=128, gamma=0.99, lam=0.95, epochs=2, minibatches=4,
-                 lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0):
+                 lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour"):
         torch = _torch()
+        if old_logp not in ("behaviour", "fp32"):
+            raise ValueError("old_logp must be 'behaviour' or 'fp32'")
+        self.old_logp = old_logp
         dev = sim.device
         self.sim = sim
         self.actor = actor if actor is not None else make_actor(device=dev, seed=seed)
@@ -158,7 +165,10 @@ class PPOTrainer:
             adv, ret = gae(rewards, values, dones, self.gamma, self.lam)
             x = feats[:T].reshape(T * N, N_FEATURES)
             a = actions.reshape(T * N)
-            old = torch.log_softmax(self.actor(x), dim=1).gather(1, a[:, None])[:, 0]
+            old32 = torch.log_softmax(self.actor(x), dim=1).gather(1, a[:, None])[:, 0]
+            behav = self.logp.reshape(T * N)  # what the kernel sampled with (bf16 actor)
+            gap = behav - old32
+            old = behav if self.old_logp == "behaviour" else old32
             adv = adv.reshape(T * N)
             adv = (adv - adv.mean()) / (adv.std() + 1e-8)
             ret = ret.reshape(T * N)
@@ -182,7 +192,8 @@ class PPOTrainer:
                 self.opt.step()
         self.rollout.refresh(self.actor)
         self.stats = {"loss": loss.detach(), "policy_loss": pg.detach(), "value_loss": vf.detach(),
-                      "entropy": ent.detach(), "mean_reward": rewards.mean()}
+                      "entropy": ent.detach(), "mean_reward": rewards.mean(), "kl_behaviour_fp32": gap.mean(),
+                      "logp_abs_diff": gap.abs().mean()}
 
     def iterate(self):
         self.update(*self.collect())
