@@ -1,0 +1,17 @@
+#!/bin/bash
+# One round's profiles of the C3 step kernel.  On the GPU box, from the repo root:
+#   tools/prof_round.sh TAG
+# (1) rocprofv3 kernel-trace/stats + FETCH_SIZE / WRITE_SIZE passes over the bench command whose
+#     roofline block they back (tools/prof_bench.sh) -> gpurun_out/prof_TAG;
+# (2) the SQ counter passes of the same kernel at 1000 ticks per launch (tools/prof_pmc.sh)
+#     -> gpurun_out/pmc_TAG.
+# Then, back in the build container, reduce them to the committed files:
+#   python3 tools/summarize_profile.py gpurun_out/prof_TAG TAG --envs 65536 --chunk 1000 \
+#       --command "python3 bench.py --no-cpu-baseline --no-extras --warmup 1000"
+#   python3 tools/pmc_table.py gpurun_out/pmc_TAG --ticks 1000 --waves 2048 --kernel k_step_n \
+#       --json profiles/TAG_sq.json --command "python3 tools/profile_driver.py --mode fused --chunk 1000 --launches 3"
+set -e
+TAG=${1:?tag}
+timeout -k 10 900 bash tools/prof_bench.sh gpurun_out/prof_$TAG --no-cpu-baseline --no-extras --warmup 1000
+timeout -k 10 900 bash tools/prof_pmc.sh gpurun_out/pmc_$TAG fused --chunk 1000 --launches 3
+echo prof_round done
