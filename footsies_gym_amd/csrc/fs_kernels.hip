@@ -231,11 +231,16 @@ __device__ __forceinline__ uint32_t raw_hist(uint32_t h, int k) {
   return k == 0 ? (b | (f << 1)) : (f | (b << 1));
 }
 
-// UpdateInput + the reads UpdateActionRequest makes of the new history.
-__device__ __forceinline__ InputEval update_input(Fighter& f, uint32_t in, int k) {
+// rel_bits as a per-lane table: entry `in` (2 bits at 2 in, for in = 0..7) of kRelLut[k], so a tick
+// spends one bit-field extract on it (the select of the lane's table is loop-invariant)
+constexpr uint32_t kRelLut0 = 0xE4E4u, kRelLut1 = 0xD8D8u;  // 3,2,1,0 / 3,1,2,0 per 4 inputs
+
+// UpdateInput + the reads UpdateActionRequest makes of the new history.  rlut = kRelLut0 / kRelLut1
+// for P1 / P2.
+__device__ __forceinline__ InputEval update_input(Fighter& f, uint32_t in, uint32_t rlut) {
   const uint32_t old_hist = f.hist;
   const int old_hold = f.hold;
-  const uint32_t r0 = rel_bits(in, k);
+  const uint32_t r0 = __builtin_amdgcn_ubfe(rlut, in << 1, 2);  // == rel_bits(in, k)
   f.hist = ((old_hist << 1) & 0xFFFEFFFEu) | (r0 & 1) | ((r0 & 2) << 15);
   f.hold = (in & IN_ATTACK) ? min(old_hold + 1, 63) : 0;
   InputEval e;
@@ -1295,7 +1300,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.rec = in;
     L.rec_count++;
   }
-  const InputEval e = update_input(L.f, in, (int)k);
+  const InputEval e = update_input(L.f, in, k ? kRelLut1 : kRelLut0);
   const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
   increment_action_frame(L.f, ai);
   // the record if the action continues, read alongside the request's ReqInfo reads; a
@@ -1327,8 +1332,8 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   asm volatile("" ::"v"(R.push), "v"(R.hurt), "v"(o_hw0), "v"(o_hw1), "v"(res), "v"(ym));
   hitbox_hurtbox_collision<FM>(L.f, k, R.hurt, o_hw0, o_hw1, res, ym);
   // the next tick's ActionInfo, issued now so its LDS latency hides behind the KO test, the
-  // reward and the stores (only the reset paths below change the action again: to STAND)
-  const AInfo ai_next = action_info<G>(L.f.act);
+  // reward and the stores (only the same-step reset below changes the action again: to STAND)
+  L.ai = action_info<G>(L.f.act);
   // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes: each
   // lane's flags (bit 0: vital 0, bit 1: guard dropped this tick; both fields are 0..3) cross
   // the pair once, then fl1 / fl2 are P1's / P2's
@@ -1360,6 +1365,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
       reset_burst<FM, P2, G>(L, true, ac);
       L.cum = 0.0;
       L.has_term = false;
+      L.ai = stand_info();  // the burst ends on STAND
     } else {
       L.pending = true;
       L.has_term = true;
@@ -1386,9 +1392,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
   st_off(o.truncated, r, (uint8_t)0);
   // all four words live until here (the tick reads three; see R.push above)
-  asm volatile("" ::"v"(ai_next));
-  // for the next tick: a same-step reset burst ended on STAND
-  L.ai = (over && p.autoreset_mode == FS_AUTORESET_SAME_STEP) ? stand_info() : ai_next;
+  asm volatile("" ::"v"(L.ai));
 }
 
 // P1's observation features for the in-kernel actor (fs_policy.h), packed bf16x2:
