@@ -22,8 +22,11 @@ HEADERS = ["fs_internal.h", "fs_tables.h", "fs_policy.h"]
 #   leaves the whole per-lane arena (272 B) in scratch memory -- 400+ scratch ops per tick.
 # -amdgpu-mfma-vgpr-form: the policy kernel's MFMA results land in VGPRs, where the tanh
 #   epilogue reads them, instead of AGPRs plus one v_accvgpr_read per element.
+# -fno-slp-vectorize: pairs of box-coordinate adds otherwise become v_pk_add_f32 plus the
+#   v_mov_b32s that line their operands up in register pairs -- more VALU issues, not fewer.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
           "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-bitwise-instead-of-logical",
+          "-fno-slp-vectorize",
           "-mllvm", "-simplifycfg-sink-common=false", "-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 

@@ -83,7 +83,7 @@ struct Fighter {
   // the fighter their world x (y == rect.y since position.y is always 0)
   int rec;        // FrameRec index of (action, frame)
   float px, ux0, ux1, hx0, hx1;
-  float pw;       // pushbox width of the record
+  float pw, phw;  // pushbox width of the record, and width / 2
 };
 
 struct Arena {
@@ -174,18 +174,6 @@ __device__ __forceinline__ float fsub(float a, float b) {
   if constexpr (FM == FS_FLOAT_DOUBLE) return (float)__dsub_rn((double)a, (double)b);
   else return __fsub_rn(a, b);
 }
-// BoxBase.xMin / xMax (F:12-13): x is the centre
-template <int FM>
-__device__ __forceinline__ float bb_xmin(float x, float w) {
-  if constexpr (FM == FS_FLOAT_DOUBLE) return (float)__dsub_rn((double)x, (double)w / 2);
-  else return __fsub_rn(x, w / 2.0f);
-}
-template <int FM>
-__device__ __forceinline__ float bb_xmax(float x, float w) {
-  if constexpr (FM == FS_FLOAT_DOUBLE) return (float)__dadd_rn((double)x, (double)w / 2);
-  else return __fadd_rn(x, w / 2.0f);
-}
-
 // ---------------------------------------------------------------------------
 // input (F:172-188, 569-666)
 // ---------------------------------------------------------------------------
@@ -413,14 +401,14 @@ __device__ __forceinline__ void update_movement(Fighter& f, float v) {
 typedef float F4 __attribute__((ext_vector_type(4)));     // native vectors: they stay in registers
 typedef uint32_t U4 __attribute__((ext_vector_type(4)));
 struct RecGeo {
-  F4 push;  // pushbox x offset, width, velocity, 0
+  F4 push;  // pushbox x offset, width, velocity, width / 2
   F4 hurt;  // hurtbox 0 (x offset, width / 2), hurtbox 1
   F4 hit;   // hitbox 0 (x offset, width / 2), hitbox 1
 };
 template <bool G>
 __device__ __forceinline__ RecGeo frame_rec(uint32_t k, uint32_t rec) {
   const Tables& T = tabs<G>();
-  const uint32_t off = __umul24(k, (uint32_t)sizeof(T.rec_push[0])) + __umul24(rec, 16u);
+  const uint32_t off = __umul24(k, (uint32_t)sizeof(T.rec_push[0])) + (rec << 4);  // rec < 64
   auto at = [&](const void* base) {
     return *reinterpret_cast<const F4*>(reinterpret_cast<const char*>(base) + off);
   };
@@ -442,6 +430,7 @@ __device__ __forceinline__ int frame_record(const Fighter& f) {
 template <int FM>
 __device__ __forceinline__ void update_boxes(Fighter& f, const RecGeo& R) {
   f.pw = R.push.y;
+  f.phw = R.push.w;
   f.px = fadd<FM>(f.x, R.push.x);
   f.ux0 = fadd<FM>(f.x, R.hurt.x);
   f.ux1 = fadd<FM>(f.x, R.hurt.z);
@@ -465,8 +454,9 @@ __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
 // bit for bit, -0.0 included), so every lane applies it.
 template <int FM>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
-  const float w = f.pw;
-  const float xmin = bb_xmin<FM>(f.px, w), xmax = bb_xmax<FM>(f.px, w);
+  // BoxBase xMin / xMax (F:12-13) with the record's exact width / 2 (w / 2 is exact in binary32,
+  // and (double)(w / 2) == (double)w / 2 for the binary64 model)
+  const float xmin = fsub<FM>(f.px, f.phw), xmax = fadd<FM>(f.px, f.phw);
   float d_lo = fsub<FM>(-kStageHalf, xmin), d_hi = fsub<FM>(kStageHalf, xmax);
   asm volatile("" : "+v"(d_lo), "+v"(d_hi));  // both computed: selects, not a branch
   const float dx = xmin < -kStageHalf ? d_lo : (xmax > kStageHalf ? d_hi : -0.0f);
@@ -841,6 +831,16 @@ __device__ __forceinline__ uint32_t xpair(uint32_t v) {
 }
 __device__ __forceinline__ int xpair(int v) { return (int)xpair((uint32_t)v); }
 __device__ __forceinline__ float xpair(float v) { return __uint_as_float(xpair(__float_as_uint(v))); }
+// P1's / P2's value of the pair on both lanes (quad_perm [0,0,2,2] / [1,1,3,3]): one DPP move
+// instead of an exchange plus a lane-parity select
+__device__ __forceinline__ uint32_t xp1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0 /* quad_perm(0,0,2,2) */, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t xp2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5 /* quad_perm(1,1,3,3) */, 0xF, 0xF, true);
+}
+__device__ __forceinline__ float xp1(float v) { return __uint_as_float(xp1(__float_as_uint(v))); }
+__device__ __forceinline__ float xp2(float v) { return __uint_as_float(xp2(__float_as_uint(v))); }
 
 struct Lane {
   Fighter f;
@@ -993,7 +993,7 @@ __device__ __forceinline__ AttackInfo attack_info(int i) {
   return a;
 }
 
-// `res` = kTables.resolve[o_rec * 4 + o_hits], read with the frame record: byte m (the box-pair
+// `res` = kTables.resolve[o_hits * kNumFrameRecs + o_rec], read with the frame record: byte m (the box-pair
 // overlap mask) holds the outcome at the attacker's hit count o_hits (low nibble) and at 0 (high).
 template <int FM>
 __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k, F4 my_hurt, float o_hw0, float o_hw1,
@@ -1016,8 +1016,7 @@ __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k,
   // (every exchange is its own statement on both lanes: inside a select the compiler may run
   // the DPP move under a one-lane exec mask, and a disabled source lane reads as 0)
   const uint32_t t1 = tab & 15u;
-  const uint32_t x1 = xpair(t1);
-  const uint32_t hitA = (k == 1 ? t1 : x1) & 1u;
+  const uint32_t hitA = xp2(t1) & 1u;  // phase A's outcome, from the P2 lane
   const uint32_t t = (k == 0 && hitA) ? (tab >> 4) : t1;  // this lane's phase as the defender
   const bool my_hit = (t & 1u) != 0;
   const int my_atk = (int)((t >> 1) & 3u);
@@ -1035,8 +1034,7 @@ __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k,
   if (!my_hit && my_prox && f.in_back) f.prox = true;  // NotifyInProximityGuardRange (F:400-406)
   // (hit, stun) of both defenders: pA = P2's (phase A), pB = P1's (phase B)
   const uint32_t mine = (uint32_t)my_hit | ((uint32_t)my_stun << 1);
-  const uint32_t other = xpair(mine);
-  const uint32_t pA = k == 1 ? mine : other, pB = k == 1 ? other : mine;
+  const uint32_t pA = xp2(mine), pB = xp1(mine);
   f.hits += k == 1 ? (int)(pB & 1u) : 0;  // NotifyAttackHit for P2
   // SetHitStun on both, phase B last (BC:576-578), as bit-mask selects (v_bfe_i32 + v_bfi_b32:
   // written as ?: the compiler branches here)
@@ -1318,7 +1316,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   const uint32_t o_hits = (uint32_t)xpair(L.f.hits);
   static_assert(kNumFrameRecs <= 64, "ybits rows are 64 records wide");
   const uint32_t ym = tabs<G>().ybits[(o_rec << 6) | (uint32_t)L.f.rec];
-  const U4 res = reinterpret_cast<const U4*>(tabs<G>().resolve)[(o_rec << 2) | o_hits];
+  const U4 res = reinterpret_cast<const U4*>(tabs<G>().resolve)[__umul24(o_hits, (uint32_t)kNumFrameRecs) + o_rec];
   update_movement<FM>(L.f, R.push.z);
   update_boxes<FM>(L.f, R);
   // the partner's hitbox half-widths (its own record's)
@@ -1327,8 +1325,8 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   push_character_vs_background<FM>(L.f);
   // consumed here, unconditionally, so the reads stay where they were issued (next to the
   // frame record) instead of being sunk into the collision's branch
-  // (R.push too: its fourth word is unused, and a register of a load in flight that the
-  // allocator considers free is reused at once, which forces a wait for the load)
+  // (R.push too: a register of a load in flight that the allocator considers free is reused at
+  // once, which forces a wait for the load)
   asm volatile("" ::"v"(R.push), "v"(R.hurt), "v"(o_hw0), "v"(o_hw1), "v"(res), "v"(ym));
   hitbox_hurtbox_collision<FM>(L.f, k, R.hurt, o_hw0, o_hw1, res, ym);
   // the next tick's ActionInfo, issued now so its LDS latency hides behind the KO test, the
@@ -1372,17 +1370,13 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     }
   } else {
     if constexpr (BOT) {  // TrainingManager.Step -> RequestNextInput -> getNextAIInput
-      const float o_x = xpair(L.f.x);
-      const uint32_t o_act = xpair((uint32_t)L.f.act);
-      const float x1 = k == 0 ? L.f.x : o_x, x2 = k == 0 ? o_x : L.f.x;
-      const uint32_t p1_act = k == 0 ? (uint32_t)L.f.act : o_act;
+      const float x1 = xp1(L.f.x), x2 = xp2(L.f.x);
+      const uint32_t p1_act = xp1((uint32_t)L.f.act);
       const uint32_t bi = bot_next_input<G>(L.bot, k, bot_distance<FM>(x1, x2), p1_act);
       L.bin = k == 1 ? bi : L.bin;
     } else if constexpr (P2 == kActors) {  // the same, for the per-arena actors
-      const float o_x = xpair(L.f.x);
-      const uint32_t o_act = xpair((uint32_t)L.f.act);
-      const float x1 = k == 0 ? L.f.x : o_x, x2 = k == 0 ? o_x : L.f.x;
-      const uint32_t p1_act = k == 0 ? (uint32_t)L.f.act : o_act, p2_act = k == 1 ? (uint32_t)L.f.act : o_act;
+      const float x1 = xp1(L.f.x), x2 = xp2(L.f.x);
+      const uint32_t p1_act = xp1((uint32_t)L.f.act), p2_act = xp2((uint32_t)L.f.act);
       actors_request<G>(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
     }
     L.has_term = false;
