@@ -707,16 +707,37 @@ __device__ __forceinline__ float bot_distance(float x1, float x2) {
 // q = this lane's queue (0 = attack on the P1 lane, 1 = movement on the P2 lane).  Both lanes of
 // the pair must call it (it exchanges with the partner); it returns the bot's input on both.
 __device__ __forceinline__ uint32_t xpair(uint32_t v);
+// The bot tables one call reads depend only on the bot's state before the call (its queue's plan
+// and index, the previous FightState's distance bucket), so the fused tick issues them at its
+// start (bot_prefetch) and the call at its end finds them resident.
+struct BotPre {
+  uint32_t code_word;  // codes[q][plan][idx >> 4]
+  BotDraw w;           // draw[q][bucket of the previous distance]
+  uint32_t len;        // len[q][plan]
+};
+__device__ __forceinline__ uint32_t bot_bucket(float d) {
+  return d > 4.0f ? 0u : d > 3.0f ? 1u : d > 2.5f ? 2u : d > 2.0f ? 3u : 4u;
+}
 template <bool G>
-__device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dist, uint32_t opp_act) {
+__device__ __forceinline__ BotPre bot_prefetch(const Bot& b, uint32_t q) {
+  const uint32_t p = b.plan != 0 ? b.plan - 1 : 0u;
+  BotPre r;
+  r.code_word = bots<G>().codes[q][p][b.idx >> 4];
+  r.w = bots<G>().draw[q][bot_bucket(b.prev_dist)];
+  r.len = bots<G>().len[q][p];
+  return r;
+}
+
+template <bool G>
+__device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dist, uint32_t opp_act, const BotPre& pre) {
   const float d = b.prev_dist;
   const uint32_t opp = b.prev_opp;
   b.prev_dist = dist;
   b.prev_opp = opp_act;
-  const uint32_t bucket = d > 4.0f ? 0u : d > 3.0f ? 1u : d > 2.5f ? 2u : d > 2.0f ? 3u : 4u;
+  const uint32_t bucket = bot_bucket(d);
   const bool busy = b.plan != 0;
   const uint32_t p = busy ? b.plan - 1 : 0u, i = b.idx;
-  const uint32_t code = (bots<G>().codes[q][p][i >> 4] >> (2 * (i & 15))) & 3u;
+  const uint32_t code = (pre.code_word >> (2 * (i & 15))) & 3u;
   const uint32_t mine = busy ? (q ? code : code << 2) : 0u;  // Left / Right bits, or IN_ATTACK
   const bool o_busy = xpair((uint32_t)busy) != 0;
   const bool mbusy = q ? busy : o_busy, abusy = q ? o_busy : busy;
@@ -728,11 +749,11 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dis
   const uint32_t x2 = rng_next(s2);
   const uint4 s0 = b.rng;
   b.rng = (dm & da) ? s2 : (dm | da) ? s1 : s0;
-  const BotDraw w = bots<G>().draw[q][bucket];
+  const BotDraw w = pre.w;
   const uint32_t drawn = (w.map >> (4 * draw_mod((!q & dm) ? x2 : x1, w))) & 15u;
   const uint32_t newp = (!q & forced) ? (uint32_t)AP_TWO_HIT : drawn;
   const uint32_t i1 = i + 1;
-  b.plan = busy ? (i1 == bots<G>().len[q][p] ? 0u : b.plan) : newp + 1;
+  b.plan = busy ? (i1 == pre.len ? 0u : b.plan) : newp + 1;
   b.idx = busy ? i1 : 0u;
   return mine | xpair(mine);
 }
@@ -1169,7 +1190,7 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko, const Actors
   L.frame_count = -1;
   L.rec_count = 0;
   if constexpr (BOT) {
-    const uint32_t bi = bot_next_input<G>(L.bot, L.k, bot_distance<FM>(x1, x2), p1_act);
+    const uint32_t bi = bot_next_input<G>(L.bot, L.k, bot_distance<FM>(x1, x2), p1_act, bot_prefetch<G>(L.bot, L.k));
     L.bin = L.k == 1 ? bi : L.bin;
   } else if constexpr (V == kActors) {
     actors_request<G>(L, ac, bot_distance<FM>(x1, x2), p1_act, p2_act);
@@ -1293,6 +1314,8 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     in = (BOT && k == 1) ? L.bin : ((P2 == FS_P2_NOOP && k == 1) ? 0u : L.act);
   }
   const int guard_before = L.f.guard;  // guards of FE._current_state
+  BotPre bpre;
+  if constexpr (BOT) bpre = bot_prefetch<G>(L.bot, k);  // consumed by this tick's bot call, at its end
   L.frame_count++;
   if (L.rec_count < kMaxRecording) {  // RecordInput (BC:593-607)
     L.rec = in;
@@ -1372,7 +1395,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     if constexpr (BOT) {  // TrainingManager.Step -> RequestNextInput -> getNextAIInput
       const float x1 = xp1(L.f.x), x2 = xp2(L.f.x);
       const uint32_t p1_act = xp1((uint32_t)L.f.act);
-      const uint32_t bi = bot_next_input<G>(L.bot, k, bot_distance<FM>(x1, x2), p1_act);
+      const uint32_t bi = bot_next_input<G>(L.bot, k, bot_distance<FM>(x1, x2), p1_act, bpre);
       L.bin = k == 1 ? bi : L.bin;
     } else if constexpr (P2 == kActors) {  // the same, for the per-arena actors
       const float x1 = xp1(L.f.x), x2 = xp2(L.f.x);
