@@ -214,11 +214,62 @@ def kat_guard_break(backend):
     assert last is not None
 
 
+PUSH_W = F32(1.4)  # F00.asset basePushBoxRect width (every walking action's pushbox uses the base rect)
+
+
+def kat_push_character(backend):
+    """Both fighters walk forward into each other (P1 Right, P2 Left) for 60 frames.  Each tick
+    moves them (F:300) and rebuilds the pushboxes at their positions (F:686-697, Rect x = position),
+    then UpdatePushCharacterVsCharacter (BC:483-501) tests the Rects (Overlaps strict:
+    r2.xMax > r1.xMin && r2.xMin < r1.xMax, xMax = width + x) and moves P1 by
+    (r1.xMax - r2.xMin) * -1 / 2 and P2 by (r1.xMax - r2.xMin) * 1 / 2 (BC:490-494), so once
+    they touch they stay pressed together, re-pushed every frame."""
+    st, _ = run(backend, lambda t: R, lambda t: L, 60)
+    x1, x2 = F32(-2), F32(2)
+    step = F32(F32(F32(2.2) * F32(1)) * DT)
+    contact = None
+    for t, s in st:
+        x1 = F32(x1 + step)
+        x2 = F32(x2 + F32(F32(F32(2.2) * F32(-1)) * DT))
+        r1_xmax, r2_xmax = F32(PUSH_W + x1), F32(PUSH_W + x2)
+        if r2_xmax > x1 and x2 < r1_xmax and x1 < x2:
+            d = F32(r1_xmax - x2)
+            x1 = F32(x1 + F32(F32(d * F32(-1)) / F32(2)))
+            x2 = F32(x2 + F32(F32(d * F32(1)) / F32(2)))
+            contact = t if contact is None else contact
+        assert s["p1Move"] == FORWARD and s["p2Move"] == FORWARD, t
+        assert s["p1Position"] == x1 and s["p2Position"] == x2, (t, s["p1Position"], x1, s["p2Position"], x2)
+    assert contact is not None and contact < 40, contact  # they met and kept being pushed apart
+
+
+def kat_push_stage(backend):
+    """P1 walks backward (Left) into the stage edge for 120 frames.  The pushbox as a BoxBase
+    is centred on the position: xMin = rect.x - rect.width / 2 (F:12); UpdatePushCharacterVsBackground
+    (BC:503-519) shifts the fighter by stageMinX - xMin whenever xMin < stageMinX = 10 * -1 / 2
+    (BattleScene battleAreaWidth 10), so P1 ends pinned with its pushbox at the wall."""
+    st, _ = run(backend, lambda t: L, lambda t: 0, 120)
+    x = F32(-2)
+    back = F32(F32(F32(1.8) * F32(1)) * DT)
+    half = F32(PUSH_W / F32(2))
+    stage_min = F32(F32(10) * F32(-1) / F32(2))
+    pinned = 0
+    for t, s in st:
+        x = F32(x - back)
+        xmin = F32(x - half)
+        if xmin < stage_min:
+            x = F32(x + F32(stage_min - xmin))
+            pinned += 1
+        assert s["p1Move"] == BACKWARD, t
+        assert s["p1Position"] == x, (t, s["p1Position"], x)
+        assert s["p2Position"] == F32(2)
+    assert pinned > 10, pinned
+
+
 ALL = {
     "idle": kat_idle, "walk": kat_walk, "n_attack_whiff": kat_n_attack_whiff, "dash_forward": kat_dash_forward,
     "dash_backward": kat_dash_backward, "charge_59": lambda b: kat_charge_special(b, 59),
     "charge_58": lambda b: kat_charge_special(b, 58), "charge_80": lambda b: kat_charge_special(b, 80),
     "proximity_guard": lambda b: kat_proximity_guard(b, True),
     "no_proximity_guard": lambda b: kat_proximity_guard(b, False), "guard_break": kat_guard_break,
-    "recording_cap": kat_recording_cap,
+    "recording_cap": kat_recording_cap, "push_character": kat_push_character, "push_stage": kat_push_stage,
 }
