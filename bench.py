@@ -228,6 +228,32 @@ def vector_env_rate(torch, N, steps, device):
     return out
 
 
+def single_env_rate(torch, steps, device):
+    """The one-arena drop-in: FootsiesEnv (the reference's own API: tuples in, dicts out) vs the
+    in-game bot, `steps` steps with random actions, auto-reset by the caller after terminal steps
+    as FE's users do.  Latency-bound by design (one launch and one D2H per step); reported beside
+    the reference's own per-game-process ceiling (<= 300 env-steps/s)."""
+    import numpy as np
+    from footsies_gym_amd.vector_env import FootsiesEnv
+    rng = np.random.default_rng(1)
+    acts = [tuple(bool(b) for b in row) for row in rng.integers(0, 2, (steps + 20, 3))]
+    env = FootsiesEnv(device=device, seed=0)
+    env.reset(seed=0)
+    for j in range(20):
+        if env.step(acts[j])[2]:
+            env.reset()
+    torch.cuda.synchronize(device)
+    t = time.perf_counter()
+    for j in range(20, 20 + steps):
+        if env.step(acts[j])[2]:
+            env.reset()
+    dt = time.perf_counter() - t
+    env.close()
+    return {"value": steps / dt, "ms_per_step": 1e3 * dt / steps, "steps": steps,
+            "config": "FootsiesEnv (1 arena, reference API: (left, right, attack) tuple in, obs/info dicts out), "
+                      "P2 = in-game bot"}
+
+
 def pmc_traffic(kernel, envs, ticks):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/*_traffic.json, written by tools/summarize_profile.py from separate
@@ -518,6 +544,10 @@ def main():
             out["vector_env"] = vector_env_rate(torch, N, min(K, 200), local)
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             out["vector_env"] = {"error": "%s: %s" % (type(e).__name__, e)}
+        try:
+            out["single_env"] = single_env_rate(torch, 500, local)
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            out["single_env"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)
     if rank == 0:
