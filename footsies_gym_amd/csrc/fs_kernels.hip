@@ -7,15 +7,16 @@
 //
 //   load (coalesced 4/8/16-B per lane) -> n ticks in registers -> store
 //
-// Frame data is one 36 KB image staged into LDS per block: per action a 16-B
-// ActionInfo (frame count, loop, cancel window), per (action, frame) an index into
-// 53 de-duplicated 96-B frame records holding every box's geometry, the velocity and
-// the hitbox attack bits -- the window scans of ActionData.cs:87-168 resolved offline
-// (tools/gen_tables.py) -- the request chain's outcome per (action, window state, inputs),
-// the box-pair y overlaps per record pair and the hit resolution per (attacker record,
-// overlap mask).  A tick's dependent LDS round trips: action info (read at the end of the
-// previous tick), then the record index and the request-table entry together, then the
-// record with the y-overlap entry, then the resolution entry.  The 180-deep input histories
+// Frame data is one 31 KB image (fs_tables.h), staged into LDS per block by the fused launches
+// and read in place from global memory by the one-tick launch: per action a 16-B ActionInfo
+// (frame count, loop, cancel window), per (action, frame) an index into 53 de-duplicated frame
+// records (three 16-B entries of x geometry and velocity) -- the window scans of
+// ActionData.cs:87-168 resolved offline (tools/gen_tables.py) -- the request chain's outcome per
+// (action, window state, inputs), the box-pair y overlaps per record pair and the hit resolution
+// per (attacker hit count, attacker record).  A tick's dependent LDS round trips: action info
+// (issued after the previous tick's collision), then the record index and the request-table
+// entry together, then the frame record with the y-overlap bits and the resolution entry.  The
+// 180-deep input histories
 // (Fighter.cs:98-101) are two 16-frame shift registers (backward / forward relative to the
 // fighter's facing) plus a saturating attack-hold counter: the reference
 // only reads input[0..16] for dashes (Fighter.cs:585-635, dashAllowFrame 9) and
@@ -41,10 +42,10 @@ constexpr int NONE = 31;  // empty buffer / reserve slot
 constexpr uint32_t IN_LEFT = 1, IN_RIGHT = 2, IN_ATTACK = 4;
 
 // ---------------------------------------------------------------------------
-// frame data staged in LDS.  Every lookup of the tick (action info -> row ->
-// box / velocity / cancel records) is a dependent, lane-divergent load; from
-// LDS it costs ~tens of cycles instead of an L1/L2 round trip.  ~4.3 KB per
-// block, copied once per launch by all threads of the block.
+// frame data staged in LDS.  Every lookup of the tick (action info -> record index and
+// request entry -> frame record) is a dependent, lane-divergent load; from LDS it costs
+// ~tens of cycles instead of an L1/L2 round trip.  31 KB per block, copied once per fused
+// launch by all threads of the block.
 // ---------------------------------------------------------------------------
 __shared__ Tables sT;
 
@@ -81,7 +82,7 @@ struct Fighter {
   bool in_back, prox, won;
   // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
   // the fighter their world x (y == rect.y since position.y is always 0)
-  int rec;        // FrameRec index of (action, frame)
+  int rec;        // frame record index of (action, frame)
   float px, ux0, ux1, hx0, hx1;
   float pw, phw;  // pushbox width of the record, and width / 2
 };
