@@ -382,9 +382,10 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def kernel_time(fn, k0, span, launches, ticks_per_launch):
+    def kernel_time(fn, lo, hi, launches, ticks_per_launch):
         """Average kernel duration with the queue pre-filled (a spin kernel holds the GPU while
-        the host enqueues), so event pairs bracket back-to-back kernels, not host gaps."""
+        the host enqueues), so event pairs bracket back-to-back kernels, not host gaps.  Every
+        launch reads action rows inside [lo, hi)."""
         torch.cuda.synchronize(dev)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
         try:
@@ -393,7 +394,7 @@ def main():
             pass
         for j, (a, b) in enumerate(evs):
             a.record()
-            fn(k0 + (j * ticks_per_launch) % max(1, span - ticks_per_launch + 1), ticks_per_launch)
+            fn(lo + (j * ticks_per_launch) % max(1, hi - lo - ticks_per_launch + 1), ticks_per_launch)
             b.record()
         torch.cuda.synchronize(dev)
         d = sorted(a.elapsed_time(b) / 1e3 for a, b in evs)
@@ -456,26 +457,26 @@ def main():
     # measured at a fixed launch shape (--roofline-ticks ticks per fs_step_n launch, the shape
     # the committed rocprofv3 summaries under profiles/ cover), independent of --steps; the
     # kernel at the timed region's own launch shape is reported beside it.
-    def roofline_at(ticks, fn, span, launches):
-        kt_, kmed_ = kernel_time(fn, W, span, launches, ticks)
+    def roofline_at(ticks, fn, lo, hi, launches):
+        kt_, kmed_ = kernel_time(fn, lo, hi, launches, ticks)
         b = N * (STATE_BYTES + ticks * STEP_IO_BYTES)
         return kt_, kmed_, b
     if args.mode == "fused":
         rt = max(1, args.roofline_ticks)
         if rt <= W + R * K and rt == chunk:
-            rfn, rspan = run_fused, W + R * K
+            rfn, rlo, rhi = run_fused, W, W + R * K
         else:
             q1, q2 = sim.hash_actions(rt, seed=args.seed ^ 0x5A5A, t0=0)
             rtraj = traj if rt == chunk else sim.alloc_trajectory(rt)
             _, rfn = make_runs(q1, q2, rtraj, rt)
-            rspan = rt
+            rlo, rhi = 0, rt
             torch.cuda.synchronize(dev)
-        kt, kmed, bytes_per_launch = roofline_at(rt, rfn, rspan, max(5, args.kernel_samples // 10))
+        kt, kmed, bytes_per_launch = roofline_at(rt, rfn, rlo, rhi, max(5, args.kernel_samples // 10))
         ticks = rt
-        st_kt, st_kmed, st_bytes = roofline_at(chunk, run_fused, W + R * K, max(5, args.kernel_samples // 5))
+        st_kt, st_kmed, st_bytes = roofline_at(chunk, run_fused, W, W + R * K, max(5, args.kernel_samples // 5))
         kname = "fsk::k_step_n<0, 0>"
     else:
-        kt, kmed, bytes_per_launch = roofline_at(1, run_step, W + R * K, args.kernel_samples)
+        kt, kmed, bytes_per_launch = roofline_at(1, run_step, W, W + R * K, args.kernel_samples)
         st_kt, st_kmed, st_bytes = kt, kmed, bytes_per_launch
         ticks = 1
         kname = "fsk::k_step<0, 0>"

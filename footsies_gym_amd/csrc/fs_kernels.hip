@@ -60,6 +60,10 @@ __device__ __forceinline__ const Tables& tabs() {
   if constexpr (G) return kTables;
   else return sT;
 }
+// Table placement of a launch (env_step's TP): all in LDS (the fused launches) or all in
+// global memory (k_step).  Measured alike for k_step: staging every table but the 17 KB request
+// table (13.5 KB per block) so that one dependent read per tick goes to L2 instead of three.
+constexpr int kTabLds = 0, kTabGlobal = 1;
 
 // ---------------------------------------------------------------------------
 // packed fighter word (u64), one per fighter in DevState::fpk
@@ -79,7 +83,7 @@ struct Fighter {
   float x;
   uint32_t hist;  // input[0..15]: bit j = backward on input[j], bit 16 + j = forward (see split_hist)
   int act, frame, stun, vital, guard, hits, buf, rsv, hold;
-  bool in_back, prox, won;
+  uint32_t in_back, prox, won;  // flags as 0 / 1 words (a carried bool is re-masked at every test)
   // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
   // the fighter their world x (y == rect.y since position.y is always 0)
   int rec;        // frame record index of (action, frame)
@@ -351,11 +355,12 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
     return took;
   }
   // reserved damage action, then buffered cancel: SetCurrentAction and return (F:212-229)
+  // (take_rsv = rsv set & no stun; take_buf = !take_rsv & buf set & (hit or whiff-cancel) & no stun,
+  // as bitwise ops: the short-circuit form materializes each condition as a 0 / 1 word)
   const int rsv = f.rsv, buf = f.buf;
-  const bool take_rsv = rsv != NONE && f.stun <= 0;
-  const bool take_buf = !take_rsv && buf != NONE && (kCanCancelOnWhiff || f.hits > 0) && f.stun <= 0;
-  const bool early = take_rsv | take_buf;
-  const int a0 = take_rsv ? rsv : buf;
+  const bool has_rsv = rsv != NONE;
+  const bool early = (f.stun <= 0) & (has_rsv | ((buf != NONE) & (kCanCancelOnWhiff | (f.hits > 0))));
+  const int a0 = has_rsv ? rsv : buf;
   // The request chain (special / attack F:234-254, dash F:256-259, movement F:265-283, each
   // through RequestAction F:472-510) as one read of kTables.req_table: its outcome depends only
   // on the action, whether it has ended or sits in its cancel window, the attack / dash / held
@@ -869,12 +874,12 @@ struct Lane {
   uint32_t k;         // 0: P1, 1: P2
   int frame_count;    // replicas ...
   uint32_t rec_count;
-  bool pending, has_term;
+  uint32_t pending, has_term;  // 0 / 1
   double cum;
   uint32_t rec;       // this player's recordingPnInput[index - 1]
   uint32_t act;       // this player's remote actor's input (TrainingRemoteActor.input)
   uint32_t bin;       // this player's bot actor's input (TrainingBattleAIActor.input), bot lanes only
-  bool p2bot;         // kActors: P2's actor is the bot (replica)
+  uint32_t p2bot;     // kActors: P2's actor is the bot (replica)
   AInfo ai;           // ActionInfo of f.act (reloaded at the end of every tick)
   Bot bot;            // FS_P2_BOT only: this lane's queue + replicas (see Bot)
   FullBot fb;         // kActors only: this fighter's whole BattleAI
@@ -1283,9 +1288,23 @@ __device__ __forceinline__ void settle_w(uint32_t& next) {
   }
 }
 
-template <int FM, int P2, int WAIT = -1, bool G = false>
+// The burst leaves mostly constants in the lane (SetupBattleStart, STAND's ActionInfo).  Where
+// the pending branch joins the tick, the compiler would materialize those constants in the join
+// block under the full exec mask -- a dozen moves on every tick of every wave, pending or not.
+// Made opaque here, they are produced inside the branch, in the registers the tick's own results
+// occupy.
+__device__ __forceinline__ void opaque_burst_results(Lane& L) {
+  asm volatile("" : "+v"(L.f.x), "+v"(L.f.act), "+v"(L.f.frame), "+v"(L.f.vital), "+v"(L.f.guard), "+v"(L.f.hits),
+               "+v"(L.f.buf), "+v"(L.f.rsv), "+v"(L.f.hold), "+v"(L.f.won), "+v"(L.f.hist));
+  asm volatile("" : "+v"(L.ai), "+v"(L.cum), "+v"(L.pending), "+v"(L.has_term), "+v"(L.frame_count),
+               "+v"(L.rec_count));
+}
+
+template <int FM, int P2, int WAIT = -1, int TP = kTabLds>
 __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next) {
   constexpr bool BOT = P2 == FS_P2_BOT;
+  constexpr bool G = TP == kTabGlobal;  // the tables from global memory: a one-tick launch (k_step),
+                                        // where no next tick reads L.ai
   const DevOutputs& o = p.out;
   const uint32_t k = L.k;
   const Actors ac{p.p1_bot != 0, p.p2_resets != 0, p.p2_noop != 0};
@@ -1300,6 +1319,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     st_off(o.reward, 8 * r, 0.0);  // per-arena outputs: both lanes store the same value (no divergent branch)
     st_off(o.terminated, r, (uint8_t)0);
     st_off(o.truncated, r, (uint8_t)0);
+    opaque_burst_results(L);
     return;
   }
   // the actor inputs of this frame (TrainingManager.p1Input/p2Input, BC:383-447): a remote
@@ -1355,7 +1375,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   hitbox_hurtbox_collision<FM>(L.f, k, R.hurt, o_hw0, o_hw1, res, ym);
   // the next tick's ActionInfo, issued now so its LDS latency hides behind the KO test, the
   // reward and the stores (only the same-step reset below changes the action again: to STAND)
-  L.ai = action_info<G>(L.f.act);
+  if constexpr (!G) L.ai = action_info<G>(L.f.act);
   // KO check (BC:212-213) and reward (FE:382-405), evaluated identically on both lanes: each
   // lane's flags (bit 0: vital 0, bit 1: guard dropped this tick; both fields are 0..3) cross
   // the pair once, then fl1 / fl2 are P1's / P2's
@@ -1410,7 +1430,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
   st_off(o.truncated, r, (uint8_t)0);
   // all four words live until here (the tick reads three; see R.push above)
-  asm volatile("" ::"v"(L.ai));
+  if constexpr (!G) asm volatile("" ::"v"(L.ai));
 }
 
 // P1's observation features for the in-kernel actor (fs_policy.h), packed bf16x2:
@@ -1529,7 +1549,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     }
   } else {
     uint32_t none = 0;
-    env_step<FM, P2, -1, true>(L, next & 7u, p, (uint32_t)a, none);
+    env_step<FM, P2, -1, kTabGlobal>(L, next & 7u, p, (uint32_t)a, none);
   }
   if (active) store_lane<P2>(L, p.st, a);
 }

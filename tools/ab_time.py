@@ -40,7 +40,8 @@ for mode in ("external", "bot"):
     d = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
     res.append(d[len(d) // 2])
     if mode == "external":  # the host-driven path: fs_step, one launch per tick (VectorEnv.step)
-        def one(k):
+        def one(k):  # action row k mod T: the rows hold T ticks
+            k %%= T
             check(lib().fs_step(sim.handle, C.c_void_p(p1.data_ptr() + k * N), q2 if q2 is None else
                                 C.c_void_p(p2.data_ptr() + k * N), _abi.FS_ACT_DEVICE), sim.handle)
         for k in range(20):
