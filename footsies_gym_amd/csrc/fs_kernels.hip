@@ -79,6 +79,11 @@ constexpr int kTabLds = 0, kTabGlobal = 1;
 //   25 ready (fightStates[5] set) | [26,29) the bot actor's last input (TrainingBattleAIActor.input)
 // ---------------------------------------------------------------------------
 
+// A pair of like box values (the x of box 0 and 1, or their half-widths): <2 x float> arithmetic is
+// one packed instruction (v_pk_add_f32), each half rounded exactly as the scalar op.
+typedef float F2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ F2 splat(float v) { return F2{v, v}; }
+
 struct Fighter {
   float x;
   uint32_t hist;  // input[0..15]: bit j = backward on input[j], bit 16 + j = forward (see split_hist)
@@ -87,7 +92,7 @@ struct Fighter {
   // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
   // the fighter their world x (y == rect.y since position.y is always 0)
   int rec;        // frame record index of (action, frame)
-  float px, ux0, ux1, hx0, hx1;
+  float px, ux0, ux1, hx0, hx1;  // world x: pushbox, hurtbox 0 / 1, hitbox 0 / 1
   float pw, phw;  // pushbox width of the record, and width / 2
 };
 
@@ -178,6 +183,16 @@ template <int FM>
 __device__ __forceinline__ float fsub(float a, float b) {
   if constexpr (FM == FS_FLOAT_DOUBLE) return (float)__dsub_rn((double)a, (double)b);
   else return __fsub_rn(a, b);
+}
+template <int FM>
+__device__ __forceinline__ F2 fadd2(F2 a, F2 b) {
+  if constexpr (FM == FS_FLOAT_DOUBLE) return F2{fadd<FM>(a.x, b.x), fadd<FM>(a.y, b.y)};
+  else return a + b;  // (-ffp-contract=off: nothing fuses into it)
+}
+template <int FM>
+__device__ __forceinline__ F2 fsub2(F2 a, F2 b) {
+  if constexpr (FM == FS_FLOAT_DOUBLE) return F2{fsub<FM>(a.x, b.x), fsub<FM>(a.y, b.y)};
+  else return a - b;
 }
 // ---------------------------------------------------------------------------
 // input (F:172-188, 569-666)
@@ -438,21 +453,24 @@ __device__ __forceinline__ void update_boxes(Fighter& f, const RecGeo& R) {
   f.pw = R.push.y;
   f.phw = R.push.w;
   f.px = fadd<FM>(f.x, R.push.x);
-  f.ux0 = fadd<FM>(f.x, R.hurt.x);
-  f.ux1 = fadd<FM>(f.x, R.hurt.z);
-  f.hx0 = fadd<FM>(f.x, R.hit.x);
-  f.hx1 = fadd<FM>(f.x, R.hit.z);
+  const F2 ux = fadd2<FM>(splat(f.x), R.hurt.xy), hx = fadd2<FM>(splat(f.x), R.hit.xy);
+  f.ux0 = ux.x;
+  f.ux1 = ux.y;
+  f.hx0 = hx.x;
+  f.hx1 = hx.y;
 }
 
 // ApplyPositionChange (F:331-350): position and every box are shifted, not rebuilt
 template <int FM>
 __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
-  f.x = fadd<FM>(f.x, dx);
-  f.px = fadd<FM>(f.px, dx);
-  f.ux0 = fadd<FM>(f.ux0, dx);
-  f.ux1 = fadd<FM>(f.ux1, dx);
-  f.hx0 = fadd<FM>(f.hx0, dx);
-  f.hx1 = fadd<FM>(f.hx1, dx);
+  const F2 xp = fadd2<FM>(F2{f.x, f.px}, splat(dx));
+  f.x = xp.x;
+  f.px = xp.y;
+  const F2 ux = fadd2<FM>(F2{f.ux0, f.ux1}, splat(dx)), hx = fadd2<FM>(F2{f.hx0, f.hx1}, splat(dx));
+  f.ux0 = ux.x;
+  f.ux1 = ux.y;
+  f.hx0 = hx.x;
+  f.hx1 = hx.y;
 }
 
 // UpdatePushCharacterVsBackground (BC:503-519) with BoxBase semantics
@@ -462,6 +480,7 @@ template <int FM>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
   // BoxBase xMin / xMax (F:12-13) with the record's exact width / 2 (w / 2 is exact in binary32,
   // and (double)(w / 2) == (double)w / 2 for the binary64 model)
+  // (xMin, xMax) as one pair: px - w/2 is px + (-w/2) bit for bit (IEEE subtraction is defined so)
   const float xmin = fsub<FM>(f.px, f.phw), xmax = fadd<FM>(f.px, f.phw);
   float d_lo = fsub<FM>(-kStageHalf, xmin), d_hi = fsub<FM>(kStageHalf, xmax);
   asm volatile("" : "+v"(d_lo), "+v"(d_hi));  // both computed: selects, not a branch
@@ -514,12 +533,11 @@ __device__ __forceinline__ int notify_damaged(Fighter& f, const AttackInfo& ad) 
 // only) and comes from kTables.ybits, which is also 0 for absent boxes (past a record's box
 // count), so no count checks are needed here.
 template <int FM>
-__device__ __forceinline__ uint32_t box_x_overlaps(float hw0, float hw1, float hx0, float hx1, float uw0, float uw1,
-                                                   float ux0, float ux1) {
+__device__ __forceinline__ uint32_t box_x_overlaps(float hw0, float hw1, float hx0, float hx1, F2 uw, F2 ux) {
   const float h0min = fsub<FM>(hx0, hw0), h0max = fadd<FM>(hx0, hw0);
   const float h1min = fsub<FM>(hx1, hw1), h1max = fadd<FM>(hx1, hw1);
-  const float u0min = fsub<FM>(ux0, uw0), u0max = fadd<FM>(ux0, uw0);
-  const float u1min = fsub<FM>(ux1, uw1), u1max = fadd<FM>(ux1, uw1);
+  const F2 umin = fsub2<FM>(ux, uw), umax = fadd2<FM>(ux, uw);  // my hurtboxes 0 / 1
+  const float u0min = umin.x, u0max = umax.x, u1min = umin.y, u1max = umax.y;
   auto ov = [](float smin, float smax, float omin, float omax) {
     return (uint32_t)((omax >= smin) & (omin <= smax));
   };
@@ -1027,7 +1045,7 @@ __device__ __forceinline__ void hitbox_hurtbox_collision(Fighter& f, uint32_t k,
                                                          U4 res, uint32_t ym) {
   // (no wave-level skip: absent hitboxes never overlap in y, ybits)
   const float o_hx0 = xpair(f.hx0), o_hx1 = xpair(f.hx1);
-  const uint32_t xm = box_x_overlaps<FM>(o_hw0, o_hw1, o_hx0, o_hx1, my_hurt.y, my_hurt.w, f.ux0, f.ux1);
+  const uint32_t xm = box_x_overlaps<FM>(o_hw0, o_hw1, o_hx0, o_hx1, my_hurt.zw, F2{f.ux0, f.ux1});
   // phase A (P1 attacks P2) is resolved on the P2 lane; its outcome crosses to P1, whose lane
   // then resolves phase B (P2 attacks P1) with P2's hit count after phase A
   // the resolution for both phases from one byte of the attacker's entry (kTables.resolve,
@@ -1364,7 +1382,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   update_movement<FM>(L.f, R.push.z);
   update_boxes<FM>(L.f, R);
   // the partner's hitbox half-widths (its own record's)
-  const float o_hw0 = xpair(R.hit.y), o_hw1 = xpair(R.hit.w);
+  const float o_hw0 = xpair(R.hit.z), o_hw1 = xpair(R.hit.w);
   push_character_vs_character<FM>(L.f, k);
   push_character_vs_background<FM>(L.f);
   // consumed here, unconditionally, so the reads stay where they were issued (next to the
