@@ -760,7 +760,7 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dis
   b.prev_opp = opp_act;
   const uint32_t bucket = bot_bucket(d);
   const bool busy = b.plan != 0;
-  const uint32_t p = busy ? b.plan - 1 : 0u, i = b.idx;
+  const uint32_t i = b.idx;  // (the plan's code word and length came with the prefetch)
   const uint32_t code = (pre.code_word >> (2 * (i & 15))) & 3u;
   const uint32_t mine = busy ? (q ? code : code << 2) : 0u;  // Left / Right bits, or IN_ATTACK
   const bool o_busy = xpair((uint32_t)busy) != 0;

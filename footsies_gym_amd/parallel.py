@@ -99,8 +99,9 @@ def gather_records_to(rec, dst=0, group=None, shard_sizes=None):
     starts = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
     dev = rec.device
     rec = _on_backend(rec.contiguous(), group)
-    if rank != dst:
-        dist.send(rec, dst, group=group)
+    if rank != dst:  # (a batch on every rank: with RCCL, the first P2P batch of a group must include all ranks)
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, rec, dst, group=group)]):
+            w.wait()
         return None
     out = torch.empty((int(starts[-1]), RECORD_BYTES), dtype=rec.dtype, device=rec.device)
     out[starts[rank]:starts[rank + 1]] = rec
