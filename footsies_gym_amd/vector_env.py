@@ -23,6 +23,10 @@ try:  # pragma: no cover - depends on the environment
     from gymnasium.vector import VectorEnv as _VectorEnvBase  # a gymnasium.vector.VectorEnv when importable
 except Exception:  # gymnasium is not installed in this image
     _VectorEnvBase = object
+try:
+    from gymnasium import Env as _EnvBase  # FootsiesEnv is a gymnasium.Env when importable (FE:20)
+except Exception:
+    _EnvBase = object
 
 
 def obs_info_from_outputs(out, prefix=""):
@@ -252,14 +256,21 @@ class FootsiesVectorEnv(_VectorEnvBase):
         self.close()
 
 
-class FootsiesEnv:
+class FootsiesEnv(_EnvBase):
     """Single-environment adapter with the reference FootsiesEnv API (FE:20-578) over
-    one arena: tuples of Python ints/floats in, reference-shaped dicts out."""
+    one arena: tuples of Python ints/floats in, reference-shaped dicts out.  A
+    ``gymnasium.Env`` subclass whenever gymnasium is importable (its reset / step / close are
+    overridden here)."""
 
     metadata = {"render_modes": "human", "render_fps": 60}
+    render_mode = None  # rendering is the Unity window's (out of scope)
+    spec = None
 
     def __init__(self, frame_delay=0, dense_reward=True, opponent=None, device=0, seed=0, by_example=False,
-                 **_unused):
+                 render_mode=None, **_unused):
+        # FE:133-134; "human" rendering is the Unity window's: accepted and recorded, nothing is drawn
+        assert render_mode is None or render_mode in self.metadata["render_modes"]
+        self.render_mode = render_mode
         self._opp = opponent
         # next_step auto-reset keeps FE's handshake: a terminal step() returns the terminal
         # obs and the agent's reset() then finds the game already at state(-1) (no RESET)

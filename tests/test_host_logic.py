@@ -118,3 +118,35 @@ def test_vector_env_subclasses_gymnasium_vector_env_when_importable(monkeypatch)
         monkeypatch.undo()
         importlib.reload(ve)
     assert ve.FootsiesVectorEnv.__mro__[1] is object
+
+
+def test_footsies_env_subclasses_gymnasium_env_when_importable(monkeypatch):
+    """With gymnasium importable, the single-arena FootsiesEnv is a gymnasium.Env (FE:20; a
+    stand-in module here) and keeps its own reset / step / close."""
+    import importlib
+    import sys
+    import types
+    gym = types.ModuleType("gymnasium")
+    vec = types.ModuleType("gymnasium.vector")
+
+    class Env:
+        def step(self, action):
+            raise AssertionError("base step called")
+
+    class VectorEnv:
+        pass
+
+    gym.Env, vec.VectorEnv, gym.vector = Env, VectorEnv, vec
+    monkeypatch.setitem(sys.modules, "gymnasium", gym)
+    monkeypatch.setitem(sys.modules, "gymnasium.vector", vec)
+    import footsies_gym_amd.vector_env as ve
+    try:
+        mod = importlib.reload(ve)
+        assert issubclass(mod.FootsiesEnv, Env)
+        for name in ("reset", "step", "close"):
+            assert getattr(mod.FootsiesEnv, name) is not getattr(Env, name, None)
+        assert mod.FootsiesEnv.render_mode is None and mod.FootsiesEnv.metadata["render_fps"] == 60
+    finally:
+        monkeypatch.undo()
+        importlib.reload(ve)
+    assert ve.FootsiesEnv.__mro__[1] is object
