@@ -423,8 +423,8 @@ typedef float F4 __attribute__((ext_vector_type(4)));     // native vectors: the
 typedef uint32_t U4 __attribute__((ext_vector_type(4)));
 struct RecGeo {
   F4 push;  // pushbox x offset, width, velocity, width / 2
-  F4 hurt;  // hurtbox 0 (x offset, width / 2), hurtbox 1
-  F4 hit;   // hitbox 0 (x offset, width / 2), hitbox 1
+  F4 hurt;  // hurtbox 0 / 1 x offsets, hurtbox 0 / 1 width / 2 (.xy / .zw: packed-f32 pairs)
+  F4 hit;   // hitbox 0 / 1 x offsets, hitbox 0 / 1 width / 2
 };
 template <bool G>
 __device__ __forceinline__ RecGeo frame_rec(uint32_t k, uint32_t rec) {
