@@ -43,6 +43,7 @@ def make_critic(hidden=64, device=None, seed=1):
 
 
 _WGRAD_CHUNK = 8192
+_SHUFFLE_CHUNK = 2048  # minibatches are drawn as shuffled runs of this many consecutive samples
 
 
 def _weight_grad(g, x):
@@ -78,7 +79,8 @@ def _linear_fn():
         def backward(ctx, gy):
             x, w = ctx.saved_tensors
             gy = gy.contiguous()
-            return gy @ w, _weight_grad(gy, x.contiguous()), gy.sum(0)
+            gx = gy @ w if ctx.needs_input_grad[0] else None  # (the first layer's input is data)
+            return gx, _weight_grad(gy, x.contiguous()), gy.sum(0)
 
     return SkinnyLinear
 
@@ -173,18 +175,26 @@ class PPOTrainer:
             adv = (adv - adv.mean()) / (adv.std() + 1e-8)
             ret = ret.reshape(T * N)
         M = T * N
-        mb = (M + self.minibatches - 1) // self.minibatches
+        # Minibatches: a random permutation of runs of _SHUFFLE_CHUNK consecutive samples (one tick,
+        # that many consecutive arenas) when they tile the batch, so each minibatch is gathered as
+        # whole runs (row copies) instead of 2 M scattered rows; per-sample otherwise.
+        C = _SHUFFLE_CHUNK if M % (_SHUFFLE_CHUNK * self.minibatches) == 0 else 1
+        rows = torch.cat([x, a[:, None].float(), old[:, None], adv[:, None], ret[:, None]], dim=1)  # [M, 12]
+        runs = rows.view(M // C, C, rows.shape[1])
+        nb = (M // C + self.minibatches - 1) // self.minibatches
         for _ in range(self.epochs):
-            perm = torch.randperm(M, device=x.device, generator=self.gen)
-            for i in range(0, M, mb):
-                idx = perm[i:i + mb]
-                logits = mlp(self.actor, x[idx])
+            perm = torch.randperm(M // C, device=x.device, generator=self.gen)
+            for i in range(0, M // C, nb):
+                b = runs[perm[i:i + nb]].view(-1, rows.shape[1])
+                xb, ab = b[:, :N_FEATURES], b[:, N_FEATURES].long()
+                oldb, advb, retb = b[:, N_FEATURES + 1], b[:, N_FEATURES + 2], b[:, N_FEATURES + 3]
+                logits = mlp(self.actor, xb)
                 lp_all = torch.log_softmax(logits, dim=1)
-                lp = lp_all.gather(1, a[idx, None])[:, 0]
-                ratio = torch.exp(lp - old[idx])
-                s1, s2 = ratio * adv[idx], torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv[idx]
+                lp = lp_all.gather(1, ab[:, None])[:, 0]
+                ratio = torch.exp(lp - oldb)
+                s1, s2 = ratio * advb, torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * advb
                 pg = -torch.min(s1, s2).mean()
-                vf = (mlp(self.critic, x[idx]).squeeze(-1) - ret[idx]).pow(2).mean()
+                vf = (mlp(self.critic, xb).squeeze(-1) - retb).pow(2).mean()
                 ent = -(lp_all.exp() * lp_all).sum(1).mean()
                 loss = pg + self.vf_coef * vf - self.ent_coef * ent
                 self.opt.zero_grad(set_to_none=True)
