@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (whole node) at 65 536 envs; bit-exact vs Unity ref"
+MI355X_SIMDS = 256 * 4  # CUs x SIMDs per CU (MI355X_MICROARCH.md)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (8.0 TB/s spec)
 STATE_BYTES = 96        # per arena per launch: 48 B state read + 48 B written (fs_kernels.hip layout)
 STEP_IO_BYTES = 40      # per env-step: 2 B actions in + 38 B outputs out (include/footsies.h fs_outputs)
@@ -274,11 +275,12 @@ def pmc_traffic(kernel, envs, ticks):
 def issue_profile(kernel, envs, ticks):
     """The step kernel's instruction-issue picture from the committed SQ counter summary
     (profiles/*_sq.json, tools/pmc_table.py --json over tools/prof_pmc.sh passes of the same
-    kernel at the same arena count): instructions issued per wave-tick, wave cycles per
-    wave-tick (quad-cycles) and their quotient, the fraction of one wave's issue ceiling (one
-    instruction per 4 cycles, MI355X_MICROARCH.md constants table) that the kernel sustains.
-    Reported beside the HBM roofline: this kernel is bound by its instruction stream, not by
-    bytes.  None when no summary matches."""
+    kernel at the same arena count): instructions issued per wave-tick and wave cycles per
+    wave-tick (quad-cycles); `frac` = the share of the SIMDs' VALU issue slots in use (one VALU
+    instruction per SIMD per 4 cycles, MI355X_MICROARCH.md), `wave_issue_frac` = one wave's
+    issued instructions over its quad-cycles.  Reported beside the HBM roofline: this kernel is
+    bound by its instruction stream and its LDS chain, not by bytes.  None when no summary
+    matches."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))):
@@ -287,12 +289,19 @@ def issue_profile(kernel, envs, ticks):
         for k in doc.get("kernels", []):
             if k["kernel"] == kernel and k["envs"] == envs:
                 pw = k["per_wave_tick"]
-                best = {"bound": "wave instruction issue (1 instruction / 4 cycles / wave)",
+                valu, qc = pw.get("SQ_INSTS_VALU", 0.0), pw.get("SQ_WAVE_CYCLES", 0.0)
+                per_simd = k.get("waves", 0) / MI355X_SIMDS  # waves sharing a SIMD's VALU slots
+                best = {"bound": "SIMD VALU issue (one VALU instruction per SIMD per 4 cycles) and each "
+                                 "wave's dependent LDS chain (DESIGN.md section 5)",
                         "insts_per_wave_tick": round(k["insts_per_wave_tick"], 1),
-                        "valu_per_wave_tick": round(pw.get("SQ_INSTS_VALU", 0.0), 1),
+                        "valu_per_wave_tick": round(valu, 1),
                         "salu_per_wave_tick": round(pw.get("SQ_INSTS_SALU", 0.0), 1),
-                        "wave_quad_cycles_per_wave_tick": round(pw.get("SQ_WAVE_CYCLES", 0.0), 1),
-                        "frac": k["wave_issue_frac"], "ticks_per_launch_profiled": k["ticks_per_launch"],
+                        "wave_quad_cycles_per_wave_tick": round(qc, 1),
+                        "waves_per_simd": per_simd,
+                        # the SIMDs' VALU issue slots in use: waves per SIMD x VALU per wave-tick
+                        # over the quad-cycles a tick takes
+                        "frac": round(per_simd * valu / qc, 3) if qc else None,
+                        "wave_issue_frac": k["wave_issue_frac"], "ticks_per_launch_profiled": k["ticks_per_launch"],
                         "source": os.path.relpath(path, ROOT)}
     return best
 
