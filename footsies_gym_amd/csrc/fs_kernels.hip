@@ -667,9 +667,11 @@ __device__ __forceinline__ const BotTables& bots() {
   else return sBot;
 }
 
-// Copy the kTables image (fs_tables.h) and the bot tables into LDS: every thread issues all
-// of its loads before any store, so the block waits for one round trip, not one per table.
-// All threads of the block must call this before any early return.
+// Copy the kTables image (fs_tables.h) and, for kernels with a scripted bot (BOTS), the bot
+// tables into LDS: every thread issues all of its loads before any store, so the block waits for
+// one round trip, not one per table.  All threads of the block must call this before any early
+// return.
+template <bool BOTS = true>
 __device__ __forceinline__ void stage_tables() {
   constexpr int kWords = sizeof(Tables) / 4;
   constexpr int kPer = (kWords + kBlock - 1) / kBlock;
@@ -682,15 +684,16 @@ __device__ __forceinline__ void stage_tables() {
     const int i = threadIdx.x + j * kBlock;
     v[j] = i < kWords ? src[i] : 0u;
   }
+  constexpr int kBotWords = sizeof(BotTables) / 4;
+  static_assert(kBotWords <= kBlock, "one bot-table word per thread");
+  const bool bot_word = BOTS && threadIdx.x < kBotWords;
+  const uint32_t bw = bot_word ? reinterpret_cast<const uint32_t*>(&kBot)[threadIdx.x] : 0u;  // with the rest
 #pragma unroll
   for (int j = 0; j < kPer; j++) {
     const int i = threadIdx.x + j * kBlock;
     if (i < kWords) dst[i] = v[j];
   }
-  constexpr int kBotWords = sizeof(BotTables) / 4;
-  static_assert(kBotWords <= kBlock, "one bot-table word per thread");
-  if (threadIdx.x < kBotWords)
-    reinterpret_cast<uint32_t*>(&sBot)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&kBot)[threadIdx.x];
+  if (bot_word) reinterpret_cast<uint32_t*>(&sBot)[threadIdx.x] = bw;
   __syncthreads();
 }
 
@@ -1491,11 +1494,22 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   // the arena state and the first action are in flight while the block stages the tables
   Lane L;
   load_lane<P2>(L, p.st, a, k);
-  uint32_t next;
-  if constexpr (FUSED && !HASH && !POL) next = row_load((reads ? src : p.p1) + (uint32_t)a);
-  else next = fetch(0);
+  // the fused loop's rows: every lane loads (so the in-flight register is written by the load
+  // alone); a lane without a row of its own reads P1's row 0, always valid in these launches,
+  // and ignores it.  Rows 0 and 1 are both in flight while the block stages the tables.
+  const int last = p.n_steps - 1;
+  const uint8_t* own = reads ? src : p.p1;
+  const uint32_t row_mul = reads ? (uint32_t)p.n_envs : 0u;
+  auto issue = [&](int t) -> uint32_t { return row_load(own + (uint32_t)min(t, last) * row_mul + (uint32_t)a); };
+  uint32_t next, row1 = 0;
+  if constexpr (FUSED && !HASH && !POL) {
+    next = issue(0);
+    row1 = issue(1);
+  } else {
+    next = fetch(0);
+  }
   if constexpr (POL) stage_policy(p.pol);
-  if constexpr (FUSED) stage_tables();
+  if constexpr (FUSED) stage_tables<P2 == FS_P2_BOT || P2 == kActors>();
   if constexpr (POL) {
     if ((l & ~63) >= 2 * p.n_envs) return;  // the whole wave is past the last arena
   } else {
@@ -1537,16 +1551,9 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       // that swap roles every tick (unrolled by two, so no register copy of a row in flight).
       // *_fl: a load in flight (read only by its wait), *_rd: the row once resident.  A load is
       // issued every tick (the last rows re-read the last one) so the wait counts hold, and the
-      // last one in flight is waited for before the wave ends.
-      const int last = p.n_steps - 1;
-      // every lane loads (so the in-flight register is written by the load alone); a lane without a
-      // row of its own reads P1's row 0, always valid in these launches, and ignores it
-      const uint8_t* own = reads ? src : p.p1;
-      const uint32_t row_mul = reads ? (uint32_t)p.n_envs : 0u;
-      auto issue = [&](int t) -> uint32_t {
-        return row_load(own + (uint32_t)min(t, last) * row_mul + (uint32_t)a);
-      };
-      uint32_t a_fl = next, b_fl = issue(1), a_rd, b_rd;
+      // last one in flight is waited for before the wave ends.  (Rows 0 and 1 were issued before
+      // the table staging.)
+      uint32_t a_fl = next, b_fl = row1, a_rd, b_rd;
       asm volatile("s_waitcnt vmcnt(0)\n\tv_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(a_rd), "=v"(b_rd)
                    : "v"(a_fl), "v"(b_fl) : "memory");
       int t = 0;
