@@ -668,33 +668,29 @@ __device__ __forceinline__ const BotTables& bots() {
 }
 
 // Copy the kTables image (fs_tables.h) and, for kernels with a scripted bot (BOTS), the bot
-// tables into LDS: every thread issues all of its loads before any store, so the block waits for
-// one round trip, not one per table.  All threads of the block must call this before any early
-// return.
+// tables into LDS by LDS-DMA (global_load_lds_dwordx4: L2 -> LDS with no VGPR round trip, 1 KB
+// per wave instruction, 8 per wave for the 31 KB image).  The DMA lands at a wave-uniform LDS
+// base + lane x 16, so each wave instruction fills one contiguous 1 KB piece of the image.
+// All threads of the block must call this before any early return.
+typedef __attribute__((address_space(1))) void* GlobalPtr;
+typedef __attribute__((address_space(3))) void* LdsPtr;
+template <int BYTES>
+__device__ __forceinline__ void lds_dma_copy(void* dst, const void* src) {
+  static_assert(BYTES % 16 == 0, "16-byte pieces");
+  constexpr int kChunks = BYTES / 16, kPieces = (kChunks + 63) / 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int j = wave; j < kPieces; j += kBlock / 64) {  // wave-uniform
+    const int c = j * 64 + lane;
+    if (c < kChunks)
+      __builtin_amdgcn_global_load_lds((GlobalPtr)(reinterpret_cast<const char*>(src) + c * 16),
+                                       (LdsPtr)(reinterpret_cast<char*>(dst) + j * 1024), 16, 0, 0);
+  }
+}
 template <bool BOTS = true>
 __device__ __forceinline__ void stage_tables() {
-  constexpr int kWords = sizeof(Tables) / 4;
-  constexpr int kPer = (kWords + kBlock - 1) / kBlock;
-  static_assert(sizeof(Tables) % 4 == 0, "table image must be word-sized");
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(&kTables);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(&sT);
-  uint32_t v[kPer];
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const int i = threadIdx.x + j * kBlock;
-    v[j] = i < kWords ? src[i] : 0u;
-  }
-  constexpr int kBotWords = sizeof(BotTables) / 4;
-  static_assert(kBotWords <= kBlock, "one bot-table word per thread");
-  const bool bot_word = BOTS && threadIdx.x < kBotWords;
-  const uint32_t bw = bot_word ? reinterpret_cast<const uint32_t*>(&kBot)[threadIdx.x] : 0u;  // with the rest
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const int i = threadIdx.x + j * kBlock;
-    if (i < kWords) dst[i] = v[j];
-  }
-  if (bot_word) reinterpret_cast<uint32_t*>(&sBot)[threadIdx.x] = bw;
-  __syncthreads();
+  lds_dma_copy<sizeof(Tables)>(&sT, &kTables);
+  if constexpr (BOTS) lds_dma_copy<sizeof(BotTables)>(&sBot, &kBot);
+  __syncthreads();  // (waits for the DMA: it counts on vmcnt)
 }
 
 // Random.Range(0, n) = x % n for the draw descriptor: x = h 2^16 + l, so x % n = (h (2^16 % n) + l) % n
