@@ -302,7 +302,6 @@ __device__ __forceinline__ bool ai_always_cancel(AInfo i) { return (i.y & 0xffu)
 __device__ __forceinline__ int ai_cancel_lo(AInfo i) { return (int)((i.y >> 16) & 0xffu); }
 __device__ __forceinline__ int ai_cancel_hi(AInfo i) { return (int)(i.y >> 24); }
 __device__ __forceinline__ uint32_t ai_cancel_mask(AInfo i) { return i.z; }
-__device__ __forceinline__ int ai_rec0(AInfo i) { return (int)i.w; }
 static_assert(sizeof(ActionInfo) == 16, "ActionInfo must be 16 bytes");
 
 // IncrementActionFrame (F:140-166); `ai` = ActionInfo of f.act
@@ -1274,8 +1273,7 @@ __device__ __forceinline__ uint32_t hash_action(uint64_t seed, uint64_t env, uin
 // resident before this tick's first store.  Loads and stores share one in-order
 // counter (vmcnt) on gfx9, so a wait for `next` placed after the stores (where the
 // compiler would put it, at the loop latch) would also wait for every store of the
-// tick to be acknowledged by memory.
-__device__ __forceinline__ void settle(uint32_t& next) { asm volatile("" : "+v"(next)); }
+// tick to be acknowledged by memory (settle_w below).
 
 // The fused loop's action rows, two ticks ahead, as loads the compiler does not track.  With the
 // compiler's own load the row for tick t+1 had to be resident before tick t's stores, a wait that
