@@ -276,11 +276,10 @@ def issue_profile(kernel, envs, ticks):
     """The step kernel's instruction-issue picture from the committed SQ counter summary
     (profiles/*_sq.json, tools/pmc_table.py --json over tools/prof_pmc.sh passes of the same
     kernel at the same arena count): instructions issued per wave-tick and wave cycles per
-    wave-tick (quad-cycles); `frac` = the share of the SIMDs' VALU issue slots in use (one VALU
-    instruction per SIMD per 4 cycles, MI355X_MICROARCH.md), `wave_issue_frac` = one wave's
-    issued instructions over its quad-cycles.  Reported beside the HBM roofline: this kernel is
-    bound by its instruction stream and its LDS chain, not by bytes.  None when no summary
-    matches."""
+    wave-tick (quad-cycles) and the quad-cycles parked in s_waitcnt; `frac` = one wave's issued
+    instructions over its quad-cycles, the share of its issue ceiling (one instruction per wave
+    per 4 cycles) it uses.  Reported beside the HBM roofline: this kernel is bound by each wave's
+    instruction stream and its LDS waits, not by bytes.  None when no summary matches."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))):
@@ -289,19 +288,16 @@ def issue_profile(kernel, envs, ticks):
         for k in doc.get("kernels", []):
             if k["kernel"] == kernel and k["envs"] == envs:
                 pw = k["per_wave_tick"]
-                valu, qc = pw.get("SQ_INSTS_VALU", 0.0), pw.get("SQ_WAVE_CYCLES", 0.0)
-                per_simd = k.get("waves", 0) / MI355X_SIMDS  # waves sharing a SIMD's VALU slots
-                best = {"bound": "SIMD VALU issue (one VALU instruction per SIMD per 4 cycles) and each "
-                                 "wave's dependent LDS chain (DESIGN.md section 5)",
+                best = {"bound": "each wave's own instruction issue (one instruction per wave per 4 cycles, "
+                                 "MI355X_MICROARCH.md constants table) and its exposed LDS waits (DESIGN.md section 5)",
                         "insts_per_wave_tick": round(k["insts_per_wave_tick"], 1),
-                        "valu_per_wave_tick": round(valu, 1),
+                        "valu_per_wave_tick": round(pw.get("SQ_INSTS_VALU", 0.0), 1),
                         "salu_per_wave_tick": round(pw.get("SQ_INSTS_SALU", 0.0), 1),
-                        "wave_quad_cycles_per_wave_tick": round(qc, 1),
-                        "waves_per_simd": per_simd,
-                        # the SIMDs' VALU issue slots in use: waves per SIMD x VALU per wave-tick
-                        # over the quad-cycles a tick takes
-                        "frac": round(per_simd * valu / qc, 3) if qc else None,
-                        "wave_issue_frac": k["wave_issue_frac"], "ticks_per_launch_profiled": k["ticks_per_launch"],
+                        "wave_quad_cycles_per_wave_tick": round(pw.get("SQ_WAVE_CYCLES", 0.0), 1),
+                        "wait_quad_cycles_per_wave_tick": round(pw.get("SQ_WAIT_ANY", 0.0), 1),
+                        "waves_per_simd": k.get("waves", 0) / MI355X_SIMDS,
+                        # instructions issued over the wave's quad-cycles: its issue ceiling in use
+                        "frac": k["wave_issue_frac"], "ticks_per_launch_profiled": k["ticks_per_launch"],
                         "source": os.path.relpath(path, ROOT)}
     return best
 
