@@ -336,6 +336,21 @@ class FootsiesEnv(_EnvBase):
     def most_recent_observation(self):
         return self._most_recent_observation
 
+    @staticmethod
+    def find_ports(start, step=1, stop=None):
+        """FE:590-614: three TCP ports not in use (game, opponent, remote control), scanning from
+        `start` by `step` (up to `stop`).  This environment opens no sockets; the ports matter to
+        scripts that start several reference-style instances, or the wire server (server.py)."""
+        import itertools
+        import psutil
+        used = {c.laddr.port for c in psutil.net_connections(kind="tcp4") if c.laddr}
+        candidates = itertools.count(start, step) if stop is None else range(start, stop, step)
+        free = list(itertools.islice((q for q in candidates if q not in used), 3))
+        if len(free) < 3:
+            raise RuntimeError("could not find 3 free ports for a new FOOTSIES instance (starting at %d with steps "
+                               "of %d until %s)" % (start, step, stop))
+        return {"game_port": free[0], "opponent_port": free[1], "remote_control_port": free[2]}
+
     @property
     def most_recent_info(self):
         return self._most_recent_info

@@ -2,6 +2,7 @@
 info decoding (state.py:26-36), spaces (footsies.py:157-171), and the output -> (obs, info,
 reward, ...) conversion including gymnasium 0.29 same-step final_observation."""
 import numpy as np
+import pytest
 
 from footsies_gym_amd import spaces
 from footsies_gym_amd.simulator import decode_actions, encode_actions
@@ -150,3 +151,20 @@ def test_footsies_env_subclasses_gymnasium_env_when_importable(monkeypatch):
         monkeypatch.undo()
         importlib.reload(ve)
     assert ve.FootsiesEnv.__mro__[1] is object
+
+
+def test_find_ports_returns_three_free_ports():
+    """FootsiesEnv.find_ports (FE:590-614): three distinct ports not bound by any TCP socket, and
+    a RuntimeError when the range cannot hold three."""
+    import socket
+    from footsies_gym_amd.vector_env import FootsiesEnv
+    with socket.socket() as held:
+        held.bind(("127.0.0.1", 0))
+        held.listen(1)
+        busy = held.getsockname()[1]
+        ports = FootsiesEnv.find_ports(busy, 1, busy + 50)
+        assert sorted(ports) == ["game_port", "opponent_port", "remote_control_port"]
+        vals = list(ports.values())
+        assert len(set(vals)) == 3 and busy not in vals and all(busy < v < busy + 50 for v in vals)
+        with pytest.raises(RuntimeError):
+            FootsiesEnv.find_ports(busy, 1, busy + 1)
