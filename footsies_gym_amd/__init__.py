@@ -9,6 +9,7 @@ ctypes.  Python-side surfaces:
   FootsiesEnv        single-arena adapter with the reference FootsiesEnv API
   FootsiesSim        the zero-copy handle (torch device tensors in/out)
   wrappers           vectorized counterparts of the reference's gymnasium wrappers
+  moves              the reference's FootsiesMove table (ids, durations, attack frame data)
 """
 from ._abi import MOVE_ID_TO_INDEX, MOVE_INDEX_TO_ID, MOVES  # noqa: F401
 from ._lib import FootsiesError  # noqa: F401

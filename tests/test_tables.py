@@ -86,3 +86,27 @@ def test_f00_json_re_extracts_identically_from_the_reference_assets(tmp_path):
                        env=dict(os.environ, FOOTSIES_REF="/root/reference"))
     assert r.returncode == 0, r.stderr[-2000:]
     assert out.read_bytes() == open(os.path.join(ROOT, "data", "f00.json"), "rb").read()
+
+
+def test_move_table_derives_from_the_frame_data():
+    """footsies_gym_amd.moves (the reference's moves.py surface): ids and durations are the
+    actions' own, and each attack's startup / active / recovery are the frames before, inside
+    and after its non-proximity hitbox windows in data/f00.json."""
+    import json
+    import os
+    from footsies_gym_amd.moves import FOOTSIES_MOVE_ID_TO_INDEX, FOOTSIES_MOVE_INDEX_TO_MOVE, FootsiesMove
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    acts = {a["name"]: a for a in json.load(open(os.path.join(root, "data", "f00.json")))["actions"]}
+    assert len(FOOTSIES_MOVE_INDEX_TO_MOVE) == len(acts) == 17
+    for i, m in enumerate(FOOTSIES_MOVE_INDEX_TO_MOVE):
+        a = acts[m.name]
+        hb = [h["win"] for h in a["hitboxes"] if not h["proximity"]]
+        if hb:
+            lo, hi = min(w[0] for w in hb), max(w[1] for w in hb)
+            frames = (lo, hi - lo + 1, a["frame_count"] - hi - 1)
+        else:
+            frames = (0, 0, 0)
+        v = m.value
+        assert (v.id, v.duration, v.startup, v.active, v.recovery) == (a["id"], a["frame_count"], *frames), m.name
+        assert FOOTSIES_MOVE_ID_TO_INDEX[v.id] == i
+    assert FootsiesMove.N_SPECIAL.value.startup == 11
