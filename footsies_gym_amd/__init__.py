@@ -12,7 +12,7 @@ ctypes.  Python-side surfaces:
   moves              the reference's FootsiesMove table (ids, durations, attack frame data)
 """
 from ._abi import MOVE_ID_TO_INDEX, MOVE_INDEX_TO_ID, MOVES  # noqa: F401
-from ._lib import FootsiesError  # noqa: F401
+from ._lib import FootsiesError, FootsiesGameClosedError  # noqa: F401
 
 __version__ = "0.1.0"
 

@@ -12,6 +12,11 @@ from . import _abi
 LIB_PATH = os.environ.get("FOOTSIES_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfootsies.so")
 
 
+class FootsiesGameClosedError(RuntimeError):
+    """The reference's FootsiesGameClosedError (exceptions.py:1-2): raised, as there, when an
+    environment is used after its game was closed (here: after close())."""
+
+
 class FootsiesError(RuntimeError):
     """A libfootsies call failed (code + fs_last_error message)."""
 

@@ -17,6 +17,7 @@ import numpy as np
 
 from . import _abi, battle_state
 from . import spaces as sp
+from ._lib import FootsiesGameClosedError
 from .simulator import FootsiesSim, decode_actions, encode_actions
 
 try:  # pragma: no cover - depends on the environment
@@ -132,6 +133,7 @@ class FootsiesVectorEnv(_VectorEnvBase):
         """FootsiesEnv.reset on every arena (or ``options["mask"]``).  ``seed``: int (arena i
         gets seed + i) or a sequence of N seeds -> Random.InitState of each arena's bot.
         ``options["hard"]=True`` forces the RESET command even after a terminated step."""
+        self._check_open()
         options = options or {}
         seeds = None
         if seed is not None:
@@ -177,7 +179,12 @@ class FootsiesVectorEnv(_VectorEnvBase):
             return np.zeros(self.num_envs, np.uint8)
         return self._opponent(*self._last)
 
+    def _check_open(self):
+        if self.closed:
+            raise FootsiesGameClosedError("the environment was closed")
+
     def step(self, actions):
+        self._check_open()
         p2 = self._p2_actions()
         if self.by_example:
             actions = None  # FE:522-523: the bot plays P1, the agent's action is not sent
@@ -195,6 +202,7 @@ class FootsiesVectorEnv(_VectorEnvBase):
         FootsiesEnv instances that are stepped at different times.  The returned batch
         holds, for inactive arenas, their previous observation with reward 0 and not
         terminated (numpy output)."""
+        self._check_open()
         p2 = self._p2_actions()
         if self.by_example:
             actions = None

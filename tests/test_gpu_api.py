@@ -509,3 +509,18 @@ def test_long_fused_launches_split_like_one(monkeypatch, p2):
     compare_states(runs[0][1], runs[1][1])
     one.close()
     split.close()
+
+
+def test_single_env_after_close_raises_game_closed_error():
+    """The single-arena FootsiesEnv, like the reference's, refuses use after close()."""
+    from footsies_gym_amd import FootsiesGameClosedError
+    from footsies_gym_amd.vector_env import FootsiesEnv
+    env = FootsiesEnv(seed=1)
+    env.reset()
+    env.step((False, True, False))
+    env.close()
+    env.close()  # idempotent
+    with pytest.raises(FootsiesGameClosedError):
+        env.step((False, False, True))
+    with pytest.raises(FootsiesGameClosedError):
+        env.reset()

@@ -168,3 +168,19 @@ def test_find_ports_returns_three_free_ports():
         assert len(set(vals)) == 3 and busy not in vals and all(busy < v < busy + 50 for v in vals)
         with pytest.raises(RuntimeError):
             FootsiesEnv.find_ports(busy, 1, busy + 1)
+
+
+def test_closed_env_raises_game_closed_error():
+    """After close(), reset / step / step_masked raise FootsiesGameClosedError (exceptions.py:1-2,
+    FE:292-306: what the reference raises once its game is gone), before touching the simulator."""
+    from footsies_gym_amd import FootsiesGameClosedError
+    from footsies_gym_amd.vector_env import FootsiesVectorEnv
+    env = object.__new__(FootsiesVectorEnv)
+    env.closed = True
+    with pytest.raises(FootsiesGameClosedError):
+        env.step(np.zeros(1, np.uint8))
+    with pytest.raises(FootsiesGameClosedError):
+        env.reset()
+    with pytest.raises(FootsiesGameClosedError):
+        env.step_masked(np.zeros(1, np.uint8), np.ones(1, bool))
+    assert issubclass(FootsiesGameClosedError, RuntimeError)
