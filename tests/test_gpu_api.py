@@ -12,6 +12,8 @@ from tests import wrapper_replay as wr
 from tests.gpu_backend import SimBackend, make
 from tests.parity_utils import compare_outputs, compare_states
 
+P2_MODES = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT, "noop": _abi.FS_P2_NOOP}
+
 pytestmark = pytest.mark.gpu
 
 
@@ -55,6 +57,28 @@ def test_step_n_trajectory_matches_single_steps(oracle_lib):
     compare_states(ora.state(), a.get_state())
     compare_states(ora.state(), b.get_state())
 
+
+@pytest.mark.parametrize("N,T,p2", [(1, 37, "external"), (33, 37, "bot"), (97, 64, "external"), (97, 1, "bot")])
+def test_fused_ragged_sizes_match_oracle(oracle_lib, N, T, p2):
+    """Fused launches over grids that are mostly idle lanes (1, 33, 97 arenas: one block, a
+    part-filled wave; the LDS-DMA staging still runs in every thread) and odd tick counts (the
+    loop's odd tail; one tick = the k_step path): every trajectory row and the final state equal
+    the oracle's."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(N, p2_mode=p2, seed=6)
+    ora = oracle_lib.Oracle(N, p2_mode=P2_MODES[p2], base_seed=6)
+    p1, p2a = sim.hash_actions(T, seed=91, p2=p2 == "external")
+    traj = sim.alloc_trajectory(T)
+    sim.step_n(T, p1, p2a if p2 == "external" else None, trajectory=traj)
+    torch.cuda.synchronize()
+    tr = {k: v.cpu().numpy() for k, v in traj.items()}
+    h1 = p1.cpu().numpy()
+    h2 = p2a.cpu().numpy() if p2 == "external" else None
+    for t in range(T):
+        exp = ora.step(h1[t], None if h2 is None else h2[t])
+        compare_outputs(exp, {k: v[t] for k, v in tr.items()}, step=t)
+    compare_states(ora.state(), sim.get_state())
 
 @pytest.mark.parametrize("autoreset", ["same_step", "next_step"])
 def test_frame_delay_paths_match_oracle(oracle_lib, autoreset):
