@@ -72,6 +72,7 @@ class FootsiesSim:
             raise ValueError("p1_mode must be one of %s" % list(P1_MODES))
         self.num_envs = int(num_envs)
         self.device = torch.device("cuda", device)
+        self._dev_index = self.device.index
         self.p2_mode = p2_mode
         self.p1_mode = p1_mode
         self.autoreset_mode = autoreset_mode
@@ -146,6 +147,14 @@ class FootsiesSim:
         (by_example) p1 is ignored and may be None."""
         torch = _torch()
         ext = self.p2_mode == "external"
+        # the RL loop's case first: uint8 [N] contiguous tensors on this handle's GPU, no mask
+        # (the ctypes prototype takes the raw pointers as ints; nothing is converted or copied)
+        if active is None and _fast_actions(p1, self._dev_index, self.num_envs) and (
+                _fast_actions(p2, self._dev_index, self.num_envs) if ext else p2 is None):
+            rc = lib().fs_step(self._h, p1.data_ptr(), p2.data_ptr() if ext else None, _abi.FS_ACT_DEVICE)
+            if rc:
+                check(rc, self._h)
+            return self._out
         if ext and p2 is None:
             raise ValueError("p2 actions are required when p2_mode='external'")
         if p1 is None:
@@ -278,6 +287,14 @@ def _host(a):
     if isinstance(a, torch.Tensor):
         return a.detach().cpu().numpy()
     return a
+
+
+def _fast_actions(t, dev_index, n):
+    """Device actions that fs_step can take as they are: a contiguous uint8 [n] CUDA tensor on the
+    handle's device."""
+    torch = _torch()
+    return (type(t) is torch.Tensor and t.dtype is torch.uint8 and t.is_cuda and t.get_device() == dev_index
+            and t.dim() == 1 and t.shape[0] == n and t.is_contiguous())
 
 
 def _to_device(a, device):
