@@ -120,6 +120,7 @@ class FootsiesVectorEnv(_VectorEnvBase):
                                float_mode=float_mode, autoreset_mode=autoreset_mode, seed=seed,
                                frame_delay=frame_delay, p1_mode="bot" if by_example else "external")
         self._p2_bot = np.zeros(self.num_envs, dtype=bool)  # arenas switched to the bot (set_opponent)
+        self._all_bot = False  # == self._p2_bot.all(), kept beside it (step reads it every call)
         self.single_observation_space = sp.single_observation_space()
         self.single_action_space = sp.single_action_space()
         self.observation_space = sp.batch_observation_space(self.num_envs)
@@ -164,18 +165,20 @@ class FootsiesVectorEnv(_VectorEnvBase):
             if change.any():
                 self.sim.set_p2_mode("bot", change)
             self._p2_bot |= sel
+            self._all_bot = bool(self._p2_bot.all())
         else:
             change = sel & self._p2_bot
             if change.any():
                 self.sim.set_p2_mode("external", change)
             self._p2_bot &= ~sel
+            self._all_bot = bool(self._p2_bot.all())
             self._opponent = opponent
 
     def _p2_actions(self):
         """P2's actions for a remote P2 (FE:525-527); arenas whose P2 is the bot ignore theirs."""
         if self.sim.p2_mode != "external":
             return None
-        if self._p2_bot.all() or self._opponent is None or self._last is None:
+        if self._all_bot or self._opponent is None or self._last is None:
             return np.zeros(self.num_envs, np.uint8)
         return self._opponent(*self._last)
 
@@ -236,6 +239,7 @@ class FootsiesVectorEnv(_VectorEnvBase):
         self.sim.set_state(state)
         if self.sim.p2_mode == "external":
             self._p2_bot = np.asarray(state["p2_bot"], dtype=bool).copy()
+            self._all_bot = bool(self._p2_bot.all())
 
     def save_battle_state_json(self, arena=0):
         """STATE_SAVE of one arena in the reference's BattleState JSON (battle_state.py)."""
