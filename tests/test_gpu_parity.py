@@ -146,3 +146,24 @@ def test_full_size_fused_matches_oracle(oracle_lib, n_envs, ticks, p2):
     compare_outputs(ora.outputs(), sim.outputs_numpy())
     sim.close()
     ora.close()
+
+
+@pytest.mark.parametrize("p2", ["external", "bot"])
+def test_long_horizon_c3_size_matches_oracle(oracle_lib, p2):
+    """C3's 65 536 arenas over 20 000 ticks (many rounds per arena: KOs, auto-resets, bot
+    plans, recordings) in 20 fused launches of 1 000 ticks with in-kernel hashed actions: the full
+    state of every arena and the last outputs equal the oracle's (OpenMP on the host)."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    n, launches, ticks = 65536, 20, 1000
+    p2m = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT}[p2]
+    sim = FootsiesSim(n, p2_mode=p2, seed=23)
+    ora = oracle_lib.Oracle(n, p2_mode=p2m, base_seed=23)
+    for _ in range(launches):
+        sim.step_n(ticks, None, None, action_seed=0x10C)
+    ora.step_n_hashed(launches * ticks, 0x10C)
+    torch.cuda.synchronize()
+    compare_states(ora.state(), sim.get_state())
+    compare_outputs(ora.outputs(), sim.outputs_numpy())
+    sim.close()
+    ora.close()
