@@ -1518,10 +1518,11 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     const uint32_t arena0 = (uint32_t)(l & ~63) >> 1;
     uint32_t d0, d1;
     policy_features(L, d0, d1);
+    const PolicyWeights W = policy_weights();
     for (int t = 0; t < p.n_steps; t++) {
       const uint32_t act = next;
       next = fetch(min(t + 1, p.n_steps - 1));
-      const PolicyOut po = policy_act(d0, d1, p.pol.seed, p.arena_base + arena0, p.t0 + (uint64_t)t);
+      const PolicyOut po = policy_act(W, d0, d1, p.pol.seed, p.arena_base + arena0, p.t0 + (uint64_t)t);
       if (active) {
         const uint32_t row = (uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a;
         if (k == 0) {

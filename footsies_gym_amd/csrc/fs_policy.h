@@ -134,8 +134,21 @@ struct PolicyOut {
 // wave's pair layout (lane 2a + k = fighter k of local arena a): `d0`, `d1` are this lane's
 // fighter features packed as bf16x2 (guard/3 | move/16, move_frame/55 | position/4.6).
 // Returns, on every lane, the action and log-probability of its own arena (l >> 1).
-__device__ __forceinline__ PolicyOut policy_act(uint32_t d0, uint32_t d1, uint64_t seed, uint64_t arena0,
-                                                uint64_t t) {
+// The weight fragments of this lane (sPol[.][lane]), read once per launch into registers: 17 ds_read_b128
+// per wave-tick less on the LDS pipe and none on the MFMA's operand path.
+struct PolicyWeights {
+  bf16x8 f[kPolFrags];
+};
+__device__ __forceinline__ PolicyWeights policy_weights() {
+  PolicyWeights w;
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < kPolFrags; i++) w.f[i] = sPol[i][l];
+  return w;
+}
+
+__device__ __forceinline__ PolicyOut policy_act(const PolicyWeights& W, uint32_t d0, uint32_t d1, uint64_t seed,
+                                                uint64_t arena0, uint64_t t) {
   const int l = threadIdx.x & 63, r = l & 31, h = l >> 5;
   // gather: MFMA lane r takes arena r's two fighters (pair lanes 2r, 2r + 1)
   const uint32_t p1d0 = lane_read(d0, 2 * r), p2d0 = lane_read(d0, 2 * r + 1);
@@ -156,7 +169,7 @@ __device__ __forceinline__ PolicyOut policy_act(uint32_t d0, uint32_t d1, uint64
   if (h == 0) ones[0] = ones[1] = (__bf16)1.0f;
   const f32x16 zero = {};
   // layer 1
-  f32x16 d1a = mfma(sPol[kPolA1 + 0][l], x, zero), d1b = mfma(sPol[kPolA1 + 1][l], x, zero);
+  f32x16 d1a = mfma(W.f[kPolA1 + 0], x, zero), d1b = mfma(W.f[kPolA1 + 1], x, zero);
   bf16x8 h1[2][2];
   activate(d1a, h1[0][0], h1[0][1]);
   activate(d1b, h1[1][0], h1[1][1]);
@@ -164,19 +177,19 @@ __device__ __forceinline__ PolicyOut policy_act(uint32_t d0, uint32_t d1, uint64
   bf16x8 h2[2][2];
 #pragma unroll
   for (int u = 0; u < 2; u++) {
-    f32x16 acc = mfma(sPol[kPolA2b + u][l], ones, zero);
+    f32x16 acc = mfma(W.f[kPolA2b + u], ones, zero);
 #pragma unroll
     for (int tt = 0; tt < 2; tt++)
 #pragma unroll
-      for (int s = 0; s < 2; s++) acc = mfma(sPol[kPolA2 + 4 * u + 2 * tt + s][l], h1[tt][s], acc);
+      for (int s = 0; s < 2; s++) acc = mfma(W.f[kPolA2 + 4 * u + 2 * tt + s], h1[tt][s], acc);
     activate(acc, h2[u][0], h2[u][1]);
   }
   // layer 3: logits of actions 4h .. 4h + 3 land in registers 0..3
-  f32x16 lg = mfma(sPol[kPolA3b][l], ones, zero);
+  f32x16 lg = mfma(W.f[kPolA3b], ones, zero);
 #pragma unroll
   for (int u = 0; u < 2; u++)
 #pragma unroll
-    for (int s = 0; s < 2; s++) lg = mfma(sPol[kPolA3 + 2 * u + s][l], h2[u][s], lg);
+    for (int s = 0; s < 2; s++) lg = mfma(W.f[kPolA3 + 2 * u + s], h2[u][s], lg);
   // softmax over the two halves (partner lane l ^ 32), inverse-CDF sample, log-probability
   const float m_mine = fmaxf(fmaxf(lg[0], lg[1]), fmaxf(lg[2], lg[3]));
   const float m = fmaxf(m_mine, lane_read(m_mine, l ^ 32));
