@@ -314,72 +314,26 @@ __device__ __forceinline__ void increment_action_frame(Fighter& f, AInfo ai) {
   f.frame = stunned ? f.frame : looped;
 }
 
-// RequestAction (F:472-510) as bit tests.  For the fighter's current (action, frame) the
-// 17-bit masks `take` / `buffer` hold the actions a request would switch to (the action has
-// ended; or it is alwaysCancelable and the request is another action) / would leave in
-// bufferActionID (inside the cancel window, listed in its mask, not itself).  A request
-// that switches replaces them by the new action's frame-0 masks (ReqInfo, fs_tables.h).
-struct ReqMasks {
-  uint32_t take, buffer;
-};
-
-__device__ __forceinline__ ReqMasks req_masks(const Fighter& f, AInfo ai) {
-  constexpr uint32_t kAll = (1u << kNumActions) - 1u;
-  const uint32_t self = 1u << f.act;
-  const bool ended = f.frame >= ai_frame_count(ai);
-  const bool ac = ai_always_cancel(ai);
-  const bool inwin = (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai));
-  ReqMasks m;
-  m.take = ended ? kAll : (ac ? (kAll & ~self) : 0u);
-  m.buffer = (!ended & !ac & inwin) ? (ai_cancel_mask(ai) & ~self) : 0u;
-  return m;
-}
-
-typedef uint32_t RInfo __attribute__((ext_vector_type(4)));  // ReqInfo: take0, buffer0, rec0, pad
-template <bool G>
-__device__ __forceinline__ RInfo req_info(int a) { return reinterpret_cast<const RInfo*>(tabs<G>().req)[a]; }
-
-// One RequestAction(a) of a chain; `took` / `rec` collect what SetCurrentAction did.
-__device__ __forceinline__ void request(Fighter& f, ReqMasks& m, bool& took, uint32_t& rec, int a, RInfo q,
-                                        bool valid) {
-  const bool take = valid & (((m.take >> a) & 1u) != 0);
-  const bool buffer = valid & !take & (((m.buffer >> a) & 1u) != 0);
-  f.act = take ? a : f.act;
-  f.buf = take ? NONE : (buffer ? a : f.buf);
-  m.take = take ? q.x : m.take;
-  m.buffer = take ? q.y : m.buffer;
-  rec = take ? q.z : rec;
-  took |= take;
-}
-
-// UpdateActionRequest (F:201-286): hasWon's RequestAction(WIN), the reserved / buffered early
-// returns, then the request chain as one table read; branch-free apart from the hasWon skip.
-// Returns whether SetCurrentAction ran; then *rec is the new action's frame-0 record.
+// UpdateActionRequest (F:201-286) as one read of kTables.req_table (tools/gen_tables.py runs
+// RequestAction's chain, F:472-510, offline for every case), branch-free:
+// * hasWon (F:204-208; set only between KO and the next SetupBattleStart, or by STATE_LOAD):
+//   RequestAction(WIN) against the current action's take / buffer masks, entry kReqWin + 3 act + cls;
+// * the reserved damage action, then the buffered cancel (F:212-229): SetCurrentAction(a0),
+//   entry kReqEarly + a0;
+// * otherwise the request chain (special / attack F:234-254, dash F:256-259, movement F:265-283):
+//   its outcome depends only on the action, whether it has ended or sits in its cancel window,
+//   the attack / dash / held direction inputs and the proximity latch.
+// The first two return before the latches are touched (F:263, 285).  Returns whether
+// SetCurrentAction ran; then *rec is the new action's frame-0 record.
 template <bool G>
 __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEval& e, AInfo ai, uint32_t* rec) {
-  ReqMasks m = req_masks(f, ai);
-  bool took = false;
-  uint32_t r = 0;
-  if (f.won) {  // F:204-208 (hasWon is only set between KO and the next SetupBattleStart)
-    request(f, m, took, r, A_WIN, req_info<G>(A_WIN), true);
-    f.frame = took ? 0 : f.frame;
-    f.hits = took ? 0 : f.hits;
-    f.rsv = took ? NONE : f.rsv;
-    *rec = r;
-    return took;
-  }
-  // reserved damage action, then buffered cancel: SetCurrentAction and return (F:212-229)
   // (take_rsv = rsv set & no stun; take_buf = !take_rsv & buf set & (hit or whiff-cancel) & no stun,
   // as bitwise ops: the short-circuit form materializes each condition as a 0 / 1 word)
   const int rsv = f.rsv, buf = f.buf;
   const bool has_rsv = rsv != NONE;
+  const bool won = f.won != 0;
   const bool early = (f.stun <= 0) & (has_rsv | ((buf != NONE) & (kCanCancelOnWhiff | (f.hits > 0))));
   const int a0 = has_rsv ? rsv : buf;
-  // The request chain (special / attack F:234-254, dash F:256-259, movement F:265-283, each
-  // through RequestAction F:472-510) as one read of kTables.req_table: its outcome depends only
-  // on the action, whether it has ended or sits in its cancel window, the attack / dash / held
-  // direction inputs and the proximity latch (tools/gen_tables.py runs the chain for each).  An
-  // early return reads the entry "SetCurrentAction(a0)" instead, so both paths merge alike.
   const bool ended = f.frame >= ai_frame_count(ai);
   const bool inwin = (f.frame >= ai_cancel_lo(ai)) & (f.frame <= ai_cancel_hi(ai));
   const uint32_t cls = ended ? 2u : (inwin ? 1u : 0u);
@@ -387,7 +341,9 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   // lanes that differ in action but not in inputs read different LDS banks)
   const uint32_t in8 = ((9u * cls + 3u * e.atk + e.dash) << 3) | (e.held << 1) | (uint32_t)f.prox;
   const uint32_t idx = ((uint32_t)f.act << 8) | (in8 ^ (uint32_t)f.act);
-  const uint32_t q = tabs<G>().req_table[early ? (uint32_t)(kReqEarly + a0) : idx];
+  const uint32_t sel = won ? (uint32_t)kReqWin + 3u * (uint32_t)f.act + cls
+                           : (early ? (uint32_t)(kReqEarly + a0) : idx);
+  const uint32_t q = tabs<G>().req_table[sel];
   const bool set = ((q >> 11) & 1u) != 0;  // SetCurrentAction ran (F:546-563)
   const bool bset = ((q >> 10) & 1u) != 0;
   f.act = set ? (int)(q & 31u) : f.act;
@@ -395,8 +351,9 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   f.frame = set ? 0 : f.frame;
   f.hits = set ? 0 : f.hits;
   f.rsv = set ? NONE : f.rsv;
-  f.in_back = early ? f.in_back : (e.held & 1u) != 0;  // for proximity guard (F:263)
-  f.prox = early ? f.prox : false;         // F:285
+  const bool keep = early | won;
+  f.in_back = keep ? f.in_back : (e.held & 1u);  // for proximity guard (F:263)
+  f.prox = keep ? f.prox : 0u;                   // F:285
   *rec = (q >> 12) & 255u;
   return set;
 }
@@ -1360,7 +1317,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   const InputEval e = update_input(L.f, in, k ? kRelLut1 : kRelLut0);
   const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
   increment_action_frame(L.f, ai);
-  // the record if the action continues, read alongside the request's ReqInfo reads; a
+  // the record if the action continues, read alongside the request entry; a
   // request that sets an action returns that action's frame-0 record
   const int rec_cont = frame_record<G>(L.f);
   uint32_t rec_set;
