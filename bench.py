@@ -175,19 +175,23 @@ def fused_policy_rate(torch, N, steps, device, ticks=100):
 
 def ppo_rate(torch, N, device, horizon=128, iterations=3):
     """Config C5 end to end: PPO iterations (fused rollout of `horizon` ticks with the in-kernel
-    actor, then GAE and 2 epochs x 4 minibatches of fp32 torch updates of actor and critic,
-    then the new weights copied into the kernel's buffers); P2 = bot.  One untimed warm-up
-    iteration."""
+    actor, then GAE and 2 epochs x 4 minibatches of fp32 Adam updates of actor and critic, then
+    the new weights copied into the kernel's buffers); P2 = bot.  `value` with the fused
+    learner kernel (fs_ppo_grad), `torch_learner` with the same loss through torch autograd.
+    One untimed warm-up iteration each."""
     from footsies_gym_amd.ppo import PPOTrainer
     from footsies_gym_amd.simulator import FootsiesSim
-    sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
-    tr = PPOTrainer(sim, horizon=horizon)
-    tr.train(1)
-    rate = tr.train(iterations)
-    sim.close()
-    return {"value": rate, "horizon": horizon, "iterations": iterations,
+    rates = {}
+    for learner in ("hip", "torch"):
+        sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
+        tr = PPOTrainer(sim, horizon=horizon, learner=learner)
+        tr.train(1)
+        rates[learner] = tr.train(iterations)
+        sim.close()
+    return {"value": rates["hip"], "torch_learner": rates["torch"], "horizon": horizon, "iterations": iterations,
             "config": "C5 end to end: %d arenas, PPO (fused rollout of %d ticks + GAE + 2x4 Adam minibatch "
-                      "updates of the 8-64-64-8 actor and critic), P2 = bot" % (N, horizon)}
+                      "updates of the 8-64-64-8 actor and critic, gradients by fs_ppo_grad), P2 = bot"
+                      % (N, horizon)}
 
 
 def vector_env_rate(torch, N, steps, device):

@@ -37,6 +37,8 @@ FS_RESET_IF_NEEDED = 1
 FS_RESET_SEED_ONLY = 2
 FS_MAX_FRAME_DELAY = 4096
 FS_RECORD_BYTES = 40
+FS_PPO_ACTOR_PARAMS = 5256
+FS_PPO_CRITIC_PARAMS = 4801
 
 # InputDefine (Assets/Script/InputData.cs:8-14)
 IN_LEFT, IN_RIGHT, IN_ATTACK = 1, 2, 4
@@ -94,6 +96,11 @@ class fs_policy(C.Structure):
     ]
 
 
+class fs_mlp(C.Structure):
+    _fields_ = [("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p), ("w3", C.c_void_p),
+                ("b3", C.c_void_p)]
+
+
 class fs_env_state(C.Structure):
     _fields_ = [
         ("p1Vital", C.c_int32), ("p2Vital", C.c_int32), ("p1Guard", C.c_int32), ("p2Guard", C.c_int32),
@@ -139,6 +146,9 @@ LIB_FUNCTIONS = {
     "fs_step_masked": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_n": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(fs_outputs)]),
     "fs_step_n_policy": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(fs_policy), C.c_void_p, C.POINTER(fs_outputs)]),
+    "fs_ppo_workspace_bytes": (C.c_size_t, []),
+    "fs_ppo_grad": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp), C.c_float, C.c_float,
+                              C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "fs_hash_actions": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "fs_outputs_get": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_pack_outputs": (C.c_int, [C.c_void_p, C.c_void_p]),

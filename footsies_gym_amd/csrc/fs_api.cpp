@@ -487,6 +487,28 @@ FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint
   return step_chunked(h, n, nullptr, p2_act, 0, traj, pol);
 }
 
+FS_API size_t fs_ppo_workspace_bytes(void) { return fsk::ppo_workspace_bytes(); }
+
+FS_API int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
+                       float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  if (!rows || n <= 0 || !actor || !critic || !grad_out || !loss_out || !workspace)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: rows, n > 0, both networks, outputs and workspace required");
+  if (workspace_bytes < fsk::ppo_workspace_bytes())
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: workspace of %zu bytes, %zu needed", workspace_bytes,
+                   fsk::ppo_workspace_bytes());
+  if (reinterpret_cast<uintptr_t>(rows) % 16)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: rows must be 16-byte aligned");
+  const float* const a[6] = {actor->w1, actor->b1, actor->w2, actor->b2, actor->w3, actor->b3};
+  const float* const c[6] = {critic->w1, critic->b1, critic->w2, critic->b2, critic->w3, critic->b3};
+  for (int i = 0; i < 6; ++i)
+    if (!a[i] || !c[i]) return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: all six arrays of each network required");
+  const hipError_t e = fsk::launch_ppo_grad(rows, n, a, c, clip, vf_coef, ent_coef, grad_out, loss_out, workspace,
+                                            static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_grad: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
 FS_API int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out) {
   if (!h || !p1_out || n_steps <= 0) return FS_E_INVALID;
   int rc;

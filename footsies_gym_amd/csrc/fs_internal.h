@@ -128,5 +128,10 @@ hipError_t launch_get_state(const DevState& st, fs_arena_state* dst, fs_env_stat
 hipError_t launch_set_state(const DevState& st, const fs_arena_state* src, int n, hipStream_t s);
 hipError_t launch_delay(const DelayParams& p, hipStream_t s);
 hipError_t launch_pack_records(const DevOutputs& o, void* dst, int n, hipStream_t s);
+// fs_learn.hip: the C5 learner's minibatch gradient (fs_ppo_grad)
+size_t ppo_workspace_bytes();
+hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
+                           float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
+                           hipStream_t s);
 
 }  // namespace fsk

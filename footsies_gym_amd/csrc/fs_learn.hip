@@ -1,0 +1,360 @@
+// fs_learn.hip -- the C5 learner's minibatch gradient (fs_ppo_grad): PPO's clipped-surrogate,
+// value and entropy loss of the actor 8-64-64-8 and the critic 8-64-64-1 (tanh MLPs, the
+// shapes of footsies_gym_amd/rollout.py make_actor / ppo.py make_critic), forward and backward
+// fused into one kernel per network, fp32 throughout.  The torch learner of ppo.py defines the
+// values (its loss and autograd's gradients); tests/test_gpu_learn.py compares the two.
+//
+// One wave per block, 32 samples per tile (kTile), a grid-stride loop over tiles.  The per-sample
+// phases run lane = sample with the small weights (W1, W3: 2 KB each) as wave-uniform scalar
+// operands; everything touching the 64 x 64 W2 runs lane = hidden unit with W2's row or column
+// in registers, looping over the tile's samples whose vectors are broadcast rows of an LDS stage:
+//  1 (sample) h1 = tanh(W1 x + b1), staged;      2 (unit j) h2[s][j] = tanh(W2[j] . h1[s] + b2[j]);
+//  3 (sample) output, loss gradient g3 (staged), g2 = (W3^T g3)(1 - h2^2);
+//  4 (unit j) dW3[.][j] += g3[s] h2[s][j];       g2 then replaces h2 in the stage;
+//  5 (unit i) g1 = (W2^T g2)[i] (1 - h1[i]^2), lane i's rows of dW2 (g2[s][i] h1[s]) and dW1.
+// The gradients accumulate in registers across tiles.
+// Each wave writes its partial gradient to the workspace; k_ppo_reduce sums the partials in a
+// fixed order, so the result does not depend on scheduling.  Nothing here is integer game
+// state: this is the learner beside the simulator, not part of the bit-exact path.
+#include <hip/hip_runtime.h>
+
+#include "fs_internal.h"
+
+namespace fsl {
+
+constexpr int kF = 8;          // features
+constexpr int kH = 64;         // hidden units
+constexpr int kRow = 12;       // rows: x[8], action, old log-prob, advantage, return
+constexpr int kPad = kH + 4;   // LDS row stride of the h1 / h2 stages (b128 writes spread over banks)
+#ifndef FSL_TILE
+#define FSL_TILE 32  // 32-sample tiles: a 19 KB stage, so two waves per SIMD fit the LDS
+#endif
+constexpr int kTile = FSL_TILE;  // samples per tile (lanes >= kTile idle in the per-sample phases)
+constexpr int kMaxWaves = 65536 / kTile;  // grid cap: 1024 (64-sample tiles) or 2048 waves
+
+template <int OUT>
+constexpr int n_params() { return kH * kF + kH + kH * kH + kH + OUT * kH + OUT; }
+template <int OUT>
+constexpr int partial_stride() { return (n_params<OUT>() + 3 + 3) & ~3; }  // + pg / vf / ent sums
+
+// parameter offsets in torch's parameters() order: w1, b1, w2, b2, w3, b3
+constexpr int kOffB1 = kH * kF, kOffW2 = kOffB1 + kH, kOffB2 = kOffW2 + kH * kH, kOffW3 = kOffB2 + kH;
+template <int OUT>
+constexpr int off_b3() { return kOffW3 + OUT * kH; }
+
+typedef float F2 __attribute__((ext_vector_type(2)));  // packed f32 pair (v_pk_fma_f32)
+__device__ __forceinline__ F2 fma2(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+using CPtr = const __attribute__((address_space(4))) float*;  // scalar (constant) loads
+
+struct Coef {
+  float clip, vf_coef, ent_coef, inv_n;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+#ifndef FSL_WAVES
+#define FSL_WAVES 2  // and their registers (256 per lane)
+#endif
+#if FSL_WAVES > 0
+#define FSL_OCC __attribute__((amdgpu_waves_per_eu(FSL_WAVES)))
+#else
+#define FSL_OCC
+#endif
+
+template <int OUT>
+__global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict__ rows, int64_t n, int64_t tiles,
+                                                 const float* __restrict__ w1, const float* __restrict__ b1,
+                                                 const float* __restrict__ w2, const float* __restrict__ b2,
+                                                 const float* __restrict__ w3, const float* __restrict__ b3,
+                                                 Coef c, float* __restrict__ partial) {
+  __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample
+  __shared__ float sH2[kTile][kPad];  // rows: h2, then g2
+  __shared__ float sG3[kTile][8];
+  __shared__ float sX[kTile][kF];
+
+  const int lane = threadIdx.x;
+  F2 dW2[kH / 2], dW1[kF / 2];  // lane i's rows, as pairs
+  float dW3[OUT], dB3[OUT];
+  float dB1 = 0.f, dB2 = 0.f, pg_sum = 0.f, vf_sum = 0.f, ent_sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kH / 2; ++k) dW2[k] = F2{0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < kF / 2; ++f) dW1[f] = F2{0.f, 0.f};
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) dW3[o] = dB3[o] = 0.f;
+  const float b2j = b2[lane];
+
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    // W1, B1, W3, B3: wave-uniform scalar loads, opaque per tile (hoisted out of the loop they
+    // would not fit the SGPRs); the constant address space keeps them scalar loads
+    // (W2's row / column loads of phases 2 and 5 likewise: hoisted, they would hold 128 VGPRs
+    // across the whole loop)
+    const float *w1v = w1, *b1v = b1, *w2v = w2, *w3v = w3, *b3v = b3;
+    asm volatile("" : "+s"(w1v), "+s"(b1v), "+s"(w2v), "+s"(w3v), "+s"(b3v));
+    const CPtr W1 = (CPtr)w1v, B1 = (CPtr)b1v, W3 = (CPtr)w3v, B3 = (CPtr)b3v;
+    const int64_t left = n - tile * kTile;
+    const int ns = (int)(left < kTile ? left : kTile);
+    const bool valid = lane < ns;
+
+    // ---- phase 1 (lane = sample): x -> h1, staged as rows ------------------------------------
+    float x[kF], tail[4];
+    if (lane < kTile) {
+      const float4* r = reinterpret_cast<const float4*>(rows + (tile * kTile + (valid ? lane : 0)) * kRow);
+      const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+      x[0] = r0.x; x[1] = r0.y; x[2] = r0.z; x[3] = r0.w;
+      x[4] = r1.x; x[5] = r1.y; x[6] = r1.z; x[7] = r1.w;
+      tail[0] = r2.x; tail[1] = r2.y; tail[2] = r2.z; tail[3] = r2.w;
+#pragma unroll
+      for (int f = 0; f < kF; ++f) x[f] = valid ? x[f] : 0.f;
+#pragma unroll
+      for (int j = 0; j < kH; j += 4) {
+        float h[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float a = B1[j + q];
+#pragma unroll
+          for (int f = 0; f < kF; ++f) a = fmaf(W1[(j + q) * kF + f], x[f], a);
+          h[q] = tanhf(a);
+        }
+        *reinterpret_cast<float4*>(&sH1[lane][j]) = make_float4(h[0], h[1], h[2], h[3]);
+      }
+      *reinterpret_cast<float4*>(&sX[lane][0]) = make_float4(x[0], x[1], x[2], x[3]);
+      *reinterpret_cast<float4*>(&sX[lane][4]) = make_float4(x[4], x[5], x[6], x[7]);
+    }
+    __syncthreads();
+
+    // ---- phase 2 (lane = unit j): h2[s][j] = tanh(b2[j] + W2[j] . h1[s]), W2's row j in registers
+    // (packed f32 pairs: one v_pk_fma_f32 per two weights)
+    {
+      F2 w2r[kH / 2];
+#pragma unroll
+      for (int k = 0; k < kH; k += 4) {
+        const float4 w = *reinterpret_cast<const float4*>(&w2v[lane * kH + k]);
+        w2r[k / 2] = F2{w.x, w.y};
+        w2r[k / 2 + 1] = F2{w.z, w.w};
+      }
+      for (int t = 0; t < ns; ++t) {
+        F2 acc[4] = {F2{b2j, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}};  // 8 partial sums
+#pragma unroll
+        for (int k = 0; k < kH; k += 4) {
+          const float4 h = *reinterpret_cast<const float4*>(&sH1[t][k]);
+          acc[(k / 4) & 1] = fma2(w2r[k / 2], F2{h.x, h.y}, acc[(k / 4) & 1]);
+          acc[2 + ((k / 4) & 1)] = fma2(w2r[k / 2 + 1], F2{h.z, h.w}, acc[2 + ((k / 4) & 1)]);
+        }
+        const F2 a = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        sH2[t][lane] = tanhf(a.x + a.y);
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 3 (lane = sample): the output, the loss gradient g3 and g2 = (W3^T g3)(1 - h2^2)
+    float g2[kH];
+    if (lane < kTile) {
+#pragma unroll
+      for (int k = 0; k < kH; k += 4) {
+        const float4 h = *reinterpret_cast<const float4*>(&sH2[lane][k]);
+        g2[k] = h.x; g2[k + 1] = h.y; g2[k + 2] = h.z; g2[k + 3] = h.w;  // h2 for now
+      }
+      float g3[8];
+      if constexpr (OUT == 8) {
+        float z[8];
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          float a = B3[o];
+#pragma unroll
+          for (int j = 0; j < kH; ++j) a = fmaf(W3[o * kH + j], g2[j], a);
+          z[o] = a;
+        }
+        // log_softmax, then the clipped surrogate and the entropy bonus (ppo.py update)
+        float m = z[0];
+#pragma unroll
+        for (int o = 1; o < 8; ++o) m = fmaxf(m, z[o]);
+        float se = 0.f;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) se += expf(z[o] - m);
+        const float lse = m + logf(se);
+        float lp[8], p[8];
+        const int act = (int)tail[0];
+        float lp_a = 0.f, ent = 0.f;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          lp[o] = z[o] - lse;
+          p[o] = expf(lp[o]);
+          lp_a = o == act ? lp[o] : lp_a;
+          ent -= p[o] * lp[o];
+        }
+        const float adv = tail[2];
+        const float r = expf(lp_a - tail[1]);
+        const float s1 = r * adv, rc = fminf(fmaxf(r, 1.f - c.clip), 1.f + c.clip), s2 = rc * adv;
+        // torch.min's gradient goes to the smaller operand (half to each on a tie); clamp's passes
+        // inside [1 - clip, 1 + clip]
+        const float inr = (r >= 1.f - c.clip && r <= 1.f + c.clip) ? 1.f : 0.f;
+        const float wsel = s1 < s2 ? 1.f : (s1 > s2 ? inr : 0.5f + 0.5f * inr);
+        const float g_lpa = -(adv * wsel) * c.inv_n * r;
+        const float g_ent = c.ent_coef * c.inv_n;  // d(-ent_coef mean H) / d(exp(lp) lp) per term
+        float g_lp[8], gsum = 0.f;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          g_lp[o] = (o == act ? g_lpa : 0.f) + g_ent * (p[o] * lp[o] + p[o]);
+          gsum += g_lp[o];
+        }
+#pragma unroll
+        for (int o = 0; o < 8; ++o) g3[o] = valid ? g_lp[o] - p[o] * gsum : 0.f;  // log_softmax backward
+        pg_sum += valid ? -fminf(s1, s2) : 0.f;
+        ent_sum += valid ? ent : 0.f;
+      } else {
+        float v = B3[0];
+#pragma unroll
+        for (int j = 0; j < kH; ++j) v = fmaf(W3[j], g2[j], v);
+        const float d = v - tail[3];
+        g3[0] = valid ? 2.f * d * (c.vf_coef * c.inv_n) : 0.f;
+        vf_sum += valid ? d * d : 0.f;
+#pragma unroll
+        for (int o = 1; o < 8; ++o) g3[o] = 0.f;
+      }
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) dB3[o] += g3[o];
+      *reinterpret_cast<float4*>(&sG3[lane][0]) = make_float4(g3[0], g3[1], g3[2], g3[3]);
+      *reinterpret_cast<float4*>(&sG3[lane][4]) = make_float4(g3[4], g3[5], g3[6], g3[7]);
+#pragma unroll
+      for (int j = 0; j < kH; ++j) {
+        float gh = 0.f;
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) gh = fmaf(W3[o * kH + j], g3[o], gh);
+        g2[j] = gh * (1.f - g2[j] * g2[j]);  // tanh backward
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 4 (lane = unit j): dW3's column j from h2's column and g3's rows ----------------
+    for (int t = 0; t < ns; ++t) {
+      const float h2c = sH2[t][lane];
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) dW3[o] = fmaf(sG3[t][o], h2c, dW3[o]);
+    }
+    __syncthreads();
+    if (lane < kTile) {  // g2 replaces h2 in its stage
+#pragma unroll
+      for (int k = 0; k < kH; k += 4)
+        *reinterpret_cast<float4*>(&sH2[lane][k]) = make_float4(g2[k], g2[k + 1], g2[k + 2], g2[k + 3]);
+    }
+    __syncthreads();
+
+    // ---- phase 5 (lane = unit i): g1 = (W2^T g2)(1 - h1^2), dW2 / dW1 rows, db1 / db2 -----------
+    {
+      F2 w2c[kH / 2];
+#pragma unroll
+      for (int j = 0; j < kH; j += 2) w2c[j / 2] = F2{w2v[j * kH + lane], w2v[(j + 1) * kH + lane]};
+      for (int t = 0; t < ns; ++t) {
+        const float g2c = sH2[t][lane];
+        const F2 g2s = F2{g2c, g2c};
+        dB2 += g2c;
+        F2 gh[4] = {F2{0.f, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}};
+#pragma unroll
+        for (int j = 0; j < kH; j += 4) {
+          const float4 g = *reinterpret_cast<const float4*>(&sH2[t][j]);
+          const float4 h = *reinterpret_cast<const float4*>(&sH1[t][j]);
+          gh[(j / 4) & 1] = fma2(w2c[j / 2], F2{g.x, g.y}, gh[(j / 4) & 1]);
+          gh[2 + ((j / 4) & 1)] = fma2(w2c[j / 2 + 1], F2{g.z, g.w}, gh[2 + ((j / 4) & 1)]);
+          dW2[j / 2] = fma2(g2s, F2{h.x, h.y}, dW2[j / 2]);
+          dW2[j / 2 + 1] = fma2(g2s, F2{h.z, h.w}, dW2[j / 2 + 1]);
+        }
+        const F2 ga = (gh[0] + gh[1]) + (gh[2] + gh[3]);
+        const float h1c = sH1[t][lane];
+        const float g1 = (ga.x + ga.y) * (1.f - h1c * h1c);
+        dB1 += g1;
+        const float4 xa = *reinterpret_cast<const float4*>(&sX[t][0]);
+        const float4 xb = *reinterpret_cast<const float4*>(&sX[t][4]);
+        const F2 g1s = F2{g1, g1};
+        dW1[0] = fma2(g1s, F2{xa.x, xa.y}, dW1[0]);
+        dW1[1] = fma2(g1s, F2{xa.z, xa.w}, dW1[1]);
+        dW1[2] = fma2(g1s, F2{xb.x, xb.y}, dW1[2]);
+        dW1[3] = fma2(g1s, F2{xb.z, xb.w}, dW1[3]);
+      }
+    }
+    __syncthreads();  // the next tile's stage overwrites what this one read
+  }
+
+  // ---- this wave's partial gradient --------------------------------------------------------
+  float* out = partial + (size_t)blockIdx.x * partial_stride<OUT>();
+#pragma unroll
+  for (int f = 0; f < kF; ++f) out[lane * kF + f] = dW1[f / 2][f & 1];
+  out[kOffB1 + lane] = dB1;
+#pragma unroll
+  for (int k = 0; k < kH; ++k) out[kOffW2 + lane * kH + k] = dW2[k / 2][k & 1];
+  out[kOffB2 + lane] = dB2;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) out[kOffW3 + o * kH + lane] = dW3[o];
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) dB3[o] = wave_sum(dB3[o]);
+  pg_sum = wave_sum(pg_sum);
+  vf_sum = wave_sum(vf_sum);
+  ent_sum = wave_sum(ent_sum);
+  if (lane == 0) {
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) out[off_b3<OUT>() + o] = dB3[o];
+    out[n_params<OUT>() + 0] = pg_sum;
+    out[n_params<OUT>() + 1] = vf_sum;
+    out[n_params<OUT>() + 2] = ent_sum;
+  }
+}
+
+// Sum the partials of `waves` waves in a fixed order: thread (g, p) adds waves g, g + 16, ...
+// of entry p, then thread g = 0 adds the 16 sums in order.  Entries past the parameters are the
+// loss sums; they are added into loss_out scaled by 1/n.
+template <int OUT>
+__global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial, int waves,
+                                                     float* __restrict__ grad, float* __restrict__ loss, float inv_n) {
+  __shared__ float sum[16][64];
+  const int pl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + pl;
+  constexpr int P = n_params<OUT>(), S = partial_stride<OUT>();
+  float a = 0.f;
+  if (p < P + 3)
+    for (int w = g; w < waves; w += 16) a += partial[(size_t)w * S + p];
+  sum[g][pl] = a;
+  __syncthreads();
+  if (g == 0 && p < P + 3) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += sum[i][pl];
+    if (p < P) grad[p] = t;
+    else loss[p - P] += t * inv_n;
+  }
+}
+
+}  // namespace fsl
+
+namespace fsk {
+
+size_t ppo_workspace_bytes() {
+  return sizeof(float) * (size_t)fsl::kMaxWaves * (fsl::partial_stride<8>() + fsl::partial_stride<1>());
+}
+
+hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
+                           float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
+                           hipStream_t s) {
+  using namespace fsl;
+  const int64_t tiles = (n + kTile - 1) / kTile;
+  const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
+  const Coef c{clip, vf_coef, ent_coef, 1.0f / (float)n};
+  float* pa = static_cast<float*>(workspace);
+  float* pc = pa + (size_t)kMaxWaves * partial_stride<8>();
+  hipError_t e = hipMemsetAsync(loss, 0, 3 * sizeof(float), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ppo_grad<8>, dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1], actor[2],
+                     actor[3], actor[4], actor[5], c, pa);
+  hipLaunchKernelGGL(k_ppo_grad<1>, dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1], critic[2],
+                     critic[3], critic[4], critic[5], c, pc);
+  hipLaunchKernelGGL(k_ppo_reduce<8>, dim3((n_params<8>() + 3 + 63) / 64), dim3(1024), 0, s, pa, waves, grad, loss,
+                     c.inv_n);
+  hipLaunchKernelGGL(k_ppo_reduce<1>, dim3((n_params<1>() + 3 + 63) / 64), dim3(1024), 0, s, pc, waves,
+                     grad + n_params<8>(), loss, c.inv_n);
+  return hipGetLastError();
+}
+
+}  // namespace fsk

@@ -9,7 +9,11 @@ One iteration:
    the same device. The observation before tick t is the output of tick t - 1 (after a
    same-step auto-reset that is the fresh round's state, so a terminal tick's successor is
    never bootstrapped through: done masks it).
-3. `epochs` x `minibatches` clipped-surrogate updates of the actor and critic (fp32 torch).
+3. `epochs` x `minibatches` clipped-surrogate updates of the actor and critic, fp32.  With
+   `learner="hip"` (the default) each minibatch's loss and gradient come from one fused
+   forward + backward kernel per network (fs_ppo_grad, csrc/fs_learn.hip) straight into the
+   parameters' .grad; `learner="torch"` runs the same loss through torch autograd (the
+   definition the kernel is tested against, tests/test_gpu_learn.py).  Adam is torch's.
    The importance ratio's old log-probabilities are the behaviour policy's: the log-probs the
    bf16 kernel actor sampled with (`old_logp="behaviour"`, the default), or the same network
    recomputed in fp32 (`old_logp="fp32"`, first ratio exactly 1).  Either way the iteration
@@ -20,8 +24,11 @@ One iteration:
 
 Nothing leaves the GPU inside an iteration, and the simulator never waits on the host.
 """
+import ctypes as C
 import time
 
+from . import _abi
+from ._lib import check, lib
 from .rollout import N_ACTIONS, N_FEATURES, FusedPolicyRollout, make_actor, obs_features
 
 
@@ -100,6 +107,51 @@ def mlp(net, x):
     return x
 
 
+class PPOGrad:
+    """fs_ppo_grad for an actor (8-64-64-8) and a critic (8-64-64-1): each call writes the
+    minibatch gradient of PPO's loss into one flat device buffer whose views are the
+    parameters' ``.grad`` (set once here), and returns the device [3] of (policy, value,
+    entropy) loss means."""
+
+    def __init__(self, actor, critic):
+        torch = _torch()
+        nets = []
+        for net, out in ((actor, N_ACTIONS), (critic, 1)):
+            lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+            acts = [m for m in net if not isinstance(m, torch.nn.Linear)]
+            shapes = [tuple(m.weight.shape) for m in lin]
+            if shapes != [(64, N_FEATURES), (64, 64), (out, 64)] or not all(isinstance(m, torch.nn.Tanh) for m in acts):
+                raise ValueError("the fused learner takes 8-64-64-%d tanh MLPs; got %s" % (out, shapes))
+            params = [t for m in lin for t in (m.weight, m.bias)]
+            if any(t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() for t in params):
+                raise ValueError("the fused learner needs contiguous fp32 device parameters")
+            nets.append(params)
+        dev = nets[0][0].device
+        self.params = nets[0] + nets[1]
+        self.grad = torch.zeros(_abi.FS_PPO_ACTOR_PARAMS + _abi.FS_PPO_CRITIC_PARAMS, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        assert off == self.grad.numel()
+        self.loss = torch.zeros(3, dtype=torch.float32, device=dev)
+        self.workspace = torch.empty(lib().fs_ppo_workspace_bytes(), dtype=torch.uint8, device=dev)
+        self._mlps = [_abi.fs_mlp(*[t.data_ptr() for t in params]) for params in nets]
+        self.device = dev
+
+    def __call__(self, rows, clip, vf_coef, ent_coef):
+        """rows: device [n][12] fp32 (features, action, old log-prob, advantage, return)."""
+        torch = _torch()
+        if rows.dtype != torch.float32 or rows.dim() != 2 or rows.shape[1] != 12 or not rows.is_contiguous():
+            raise ValueError("rows must be a contiguous [n, 12] float32 tensor")
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().fs_ppo_grad(C.c_void_p(rows.data_ptr()), rows.shape[0], C.byref(self._mlps[0]),
+                                C.byref(self._mlps[1]), clip, vf_coef, ent_coef, C.c_void_p(self.grad.data_ptr()),
+                                C.c_void_p(self.loss.data_ptr()), C.c_void_p(self.workspace.data_ptr()),
+                                self.workspace.numel(), C.c_void_p(stream)))
+        return self.loss
+
+
 def gae(rewards, values, dones, gamma, lam):
     """Generalised advantage estimation over [T][N]: values has T + 1 rows (the last one
     bootstraps); dones[t] = 1 cuts the recursion after tick t.  Returns (advantages, returns)."""
@@ -120,10 +172,13 @@ class PPOTrainer:
     rollout, all arenas in every minibatch round."""
 
     def __init__(self, sim, actor=None, critic=None, horizon=128, gamma=0.99, lam=0.95, epochs=2, minibatches=4,
-                 lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour"):
+                 lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour", learner="hip"):
         torch = _torch()
         if old_logp not in ("behaviour", "fp32"):
             raise ValueError("old_logp must be 'behaviour' or 'fp32'")
+        if learner not in ("hip", "torch"):
+            raise ValueError("learner must be 'hip' or 'torch'")
+        self.learner = learner
         self.old_logp = old_logp
         dev = sim.device
         self.sim = sim
@@ -134,6 +189,7 @@ class PPOTrainer:
         self.epochs, self.minibatches, self.clip = epochs, minibatches, clip
         self.vf_coef, self.ent_coef = vf_coef, ent_coef
         self.opt = torch.optim.Adam(list(self.actor.parameters()) + list(self.critic.parameters()), lr=lr)
+        self._grad = PPOGrad(self.actor, self.critic) if learner == "hip" else None
         self.traj = sim.alloc_trajectory(horizon)
         n = sim.num_envs
         self.actions = torch.empty((horizon, n), dtype=torch.uint8, device=dev)
@@ -186,6 +242,10 @@ class PPOTrainer:
             perm = torch.randperm(M // C, device=x.device, generator=self.gen)
             for i in range(0, M // C, nb):
                 b = runs[perm[i:i + nb]].view(-1, rows.shape[1])
+                if self._grad is not None:  # fused forward + backward straight into .grad
+                    lm = self._grad(b, self.clip, self.vf_coef, self.ent_coef)
+                    self.opt.step()
+                    continue
                 xb, ab = b[:, :N_FEATURES], b[:, N_FEATURES].long()
                 oldb, advb, retb = b[:, N_FEATURES + 1], b[:, N_FEATURES + 2], b[:, N_FEATURES + 3]
                 logits = mlp(self.actor, xb)
@@ -201,6 +261,9 @@ class PPOTrainer:
                 loss.backward()
                 self.opt.step()
         self.rollout.refresh(self.actor)
+        if self._grad is not None:
+            pg, vf, ent = lm[0].clone(), lm[1].clone(), lm[2].clone()
+            loss = pg + self.vf_coef * vf - self.ent_coef * ent
         self.stats = {"loss": loss.detach(), "policy_loss": pg.detach(), "value_loss": vf.detach(),
                       "entropy": ent.detach(), "mean_reward": rewards.mean(), "kl_behaviour_fp32": gap.mean(),
                       "logp_abs_diff": gap.abs().mean()}
@@ -221,4 +284,4 @@ class PPOTrainer:
         return iterations * self.horizon * self.sim.num_envs / (time.perf_counter() - t0)
 
 
-__all__ = ["PPOTrainer", "make_critic", "gae", "N_ACTIONS"]
+__all__ = ["PPOTrainer", "PPOGrad", "make_critic", "gae", "N_ACTIONS"]

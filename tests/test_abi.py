@@ -43,7 +43,7 @@ def test_abi_version(lib):
 def _c_layout(tmp_path):
     structs = {"fs_config": _abi.fs_config, "fs_outputs": _abi.fs_outputs, "fs_env_state": _abi.fs_env_state,
                "fs_fighter_state": _abi.fs_fighter_state, "fs_arena_state": _abi.fs_arena_state,
-               "fs_policy": _abi.fs_policy}
+               "fs_policy": _abi.fs_policy, "fs_mlp": _abi.fs_mlp}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "footsies.h"', "int main(void){"]
     for s, cls in structs.items():
         lines.append('printf("%s size %%zu\\n", sizeof(%s));' % (s, s))

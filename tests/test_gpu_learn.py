@@ -1,0 +1,134 @@
+"""fs_ppo_grad (csrc/fs_learn.hip), the C5 learner's fused forward + backward, against torch
+autograd on the same loss (ppo.py's learner="torch" path, written out here): fp32 gradients of
+both networks and the three loss means, on ragged sample counts (a partial last 64-sample
+tile), with ratios inside and outside the clip range and a zero-advantage tie.
+
+Tolerance: the kernel and hipBLASLt sum in different orders in fp32, so each gradient tensor
+must agree to rtol 1e-4 with atol 1e-6 x that tensor's largest magnitude (measured differences
+are ~1e-6 relative).  Not a bit-exact path: this is the learner beside the simulator."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-4
+ATOL_FRAC = 1e-6
+
+
+def _nets(seed):
+    import torch
+    from footsies_gym_amd.ppo import make_critic
+    from footsies_gym_amd.rollout import make_actor
+    dev = torch.device("cuda", 0)
+    return make_actor(device=dev, seed=seed), make_critic(device=dev, seed=seed + 1)
+
+
+def _rows(actor, n, seed):
+    """[n, 12] rows whose old log-probs put ratios below, inside and above the clip range."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    dev = torch.device("cuda", 0)
+    x = torch.rand((n, 8), generator=g, device=dev) * 2 - 0.5
+    a = torch.randint(0, 8, (n,), generator=g, device=dev)
+    with torch.no_grad():
+        lp = torch.log_softmax(actor(x), dim=1).gather(1, a[:, None])[:, 0]
+    old = lp + torch.randn(n, generator=g, device=dev) * 0.3
+    adv = torch.randn(n, generator=g, device=dev)
+    adv[::17] = 0.0  # s1 == s2 == 0: torch.min's tie
+    ret = torch.randn(n, generator=g, device=dev)
+    return torch.cat([x, a[:, None].float(), old[:, None], adv[:, None], ret[:, None]], dim=1).contiguous()
+
+
+def _torch_reference(actor, critic, rows, clip, vf_coef, ent_coef):
+    """ppo.py's update loss on one minibatch, through autograd (the learner="torch" path)."""
+    import torch
+    xb, ab = rows[:, :8], rows[:, 8].long()
+    oldb, advb, retb = rows[:, 9], rows[:, 10], rows[:, 11]
+    params = list(actor.parameters()) + list(critic.parameters())
+    for p in params:
+        p.grad = None
+    lp_all = torch.log_softmax(actor(xb), dim=1)
+    lp = lp_all.gather(1, ab[:, None])[:, 0]
+    ratio = torch.exp(lp - oldb)
+    pg = -torch.min(ratio * advb, torch.clamp(ratio, 1 - clip, 1 + clip) * advb).mean()
+    vf = (critic(xb).squeeze(-1) - retb).pow(2).mean()
+    ent = -(lp_all.exp() * lp_all).sum(1).mean()
+    (pg + vf_coef * vf - ent_coef * ent).backward()
+    grads = [p.grad.detach().clone() for p in params]
+    for p in params:
+        p.grad = None
+    return grads, torch.stack([pg, vf, ent]).detach()
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 5000, 70001])
+def test_ppo_grad_matches_autograd(n):
+    import torch
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=n % 7)
+    rows = _rows(actor, n, seed=n)
+    clip, vf_coef, ent_coef = 0.2, 0.5, 0.01
+    ref, ref_loss = _torch_reference(actor, critic, rows, clip, vf_coef, ent_coef)
+    pg = PPOGrad(actor, critic)
+    loss = pg(rows, clip, vf_coef, ent_coef).clone()
+    got = [p.grad.detach().clone() for p in pg.params]
+    torch.cuda.synchronize()
+    r = torch.exp(torch.log_softmax(actor(rows[:, :8]), 1).gather(1, rows[:, 8].long()[:, None])[:, 0] - rows[:, 9])
+    if n >= 5000:  # the rows exercise both clip edges
+        assert bool((r < 1 - clip).any()) and bool((r > 1 + clip).any()) and bool(((r > 0.8) & (r < 1.2)).any())
+    names = ["actor.w1", "actor.b1", "actor.w2", "actor.b2", "actor.w3", "actor.b3",
+             "critic.w1", "critic.b1", "critic.w2", "critic.b2", "critic.w3", "critic.b3"]
+    for name, g, e in zip(names, got, ref):
+        assert g.shape == e.shape, name
+        scale = float(e.abs().max())
+        torch.testing.assert_close(g, e, rtol=RTOL, atol=ATOL_FRAC * max(scale, 1e-12), msg=name)
+    torch.testing.assert_close(loss, ref_loss, rtol=RTOL, atol=1e-6)
+
+
+def test_ppo_grad_is_deterministic_and_rejects_bad_input():
+    import torch
+    from footsies_gym_amd._lib import FootsiesError
+    from footsies_gym_amd.ppo import PPOGrad
+    from footsies_gym_amd.rollout import make_actor
+    actor, critic = _nets(seed=2)
+    rows = _rows(actor, 200_000, seed=9)
+    pg = PPOGrad(actor, critic)
+    pg(rows, 0.2, 0.5, 0.01)
+    first = pg.grad.clone()
+    pg(rows, 0.2, 0.5, 0.01)
+    assert torch.equal(first, pg.grad)  # fixed summation order: identical on every call
+    with pytest.raises(ValueError):
+        pg(rows[:, :11].contiguous(), 0.2, 0.5, 0.01)
+    with pytest.raises(FootsiesError):
+        pg(rows[:0], 0.2, 0.5, 0.01)
+    with pytest.raises(ValueError):
+        PPOGrad(make_actor(hidden=32, device=torch.device("cuda", 0)), critic)
+
+
+def test_ppo_trainer_hip_step_equals_torch_step():
+    """One minibatch update through PPOTrainer's two learners from the same weights and rows:
+    the parameters after Adam agree (Adam's first step moves each weight by ~lr * sign(grad), so
+    a sign flip of a near-zero gradient is the only way they could differ by more than
+    rounding; it is bounded by 2 lr and counted)."""
+    import torch
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=5)
+    rows = _rows(actor, 32768, seed=5)
+    lr = 1e-3
+    res = []
+    for learner in ("hip", "torch"):
+        a, c = _nets(seed=5)
+        opt = torch.optim.Adam(list(a.parameters()) + list(c.parameters()), lr=lr)
+        if learner == "hip":
+            PPOGrad(a, c)(rows, 0.2, 0.5, 0.01)
+        else:
+            grads, _ = _torch_reference(a, c, rows, 0.2, 0.5, 0.01)
+            for p, g in zip(list(a.parameters()) + list(c.parameters()), grads):
+                p.grad = g
+        opt.step()
+        res.append([p.detach().clone() for p in list(a.parameters()) + list(c.parameters())])
+    flips = 0
+    for h, t in zip(*res):
+        d = (h - t).abs()
+        assert float(d.max()) <= 2 * lr * 1.001
+        flips += int((d > 1e-6).sum())
+    total = sum(p.numel() for p in res[0])
+    assert flips <= total // 1000, (flips, total)

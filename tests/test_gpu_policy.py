@@ -162,17 +162,19 @@ def test_fused_policy_without_outputs_and_bad_args():
         FusedPolicyRollout(a, make_actor(hidden=32, device=torch.device("cuda", 0)))
 
 
-@pytest.mark.parametrize("N,horizon,iters,old", [(2048, 32, 3, "behaviour"), (2048, 32, 2, "fp32"),
-                                                 (65536, 16, 2, "behaviour")])
-def test_ppo_iterations_learn_and_refresh_the_kernel_actor(N, horizon, iters, old):
-    """PPOTrainer: fused rollouts + torch updates; losses finite, weights move, and the
+@pytest.mark.parametrize("N,horizon,iters,old,learner", [(2048, 32, 3, "behaviour", "hip"),
+                                                         (2048, 32, 2, "fp32", "hip"),
+                                                         (2048, 32, 2, "behaviour", "torch"),
+                                                         (65536, 16, 2, "behaviour", "hip")])
+def test_ppo_iterations_learn_and_refresh_the_kernel_actor(N, horizon, iters, old, learner):
+    """PPOTrainer: fused rollouts + fused-kernel (or torch autograd) updates; losses finite, weights move, and the
     kernel samples from the refreshed weights (the same seed then draws different actions).
     Every iteration reports how far the bf16 behaviour actor is from the fp32 one it trains."""
     import torch
     from footsies_gym_amd.ppo import PPOTrainer
     from footsies_gym_amd.simulator import FootsiesSim
     sim = FootsiesSim(N, p2_mode="bot", seed=5)
-    tr = PPOTrainer(sim, horizon=horizon, epochs=2, minibatches=4, lr=1e-2, seed=3, old_logp=old)
+    tr = PPOTrainer(sim, horizon=horizon, epochs=2, minibatches=4, lr=1e-2, seed=3, old_logp=old, learner=learner)
     w0 = [p.detach().clone() for p in tr.actor.parameters()]
     k0 = [p.clone() for p in tr.rollout.params]
     rate = tr.train(iters)
