@@ -56,6 +56,34 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+typedef float F16 __attribute__((ext_vector_type(16)));  // a 32 x 32 f32 MFMA accumulator
+__device__ __forceinline__ F16 mfma32(float a, float b, F16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+// Accumulator element q of lane (r, hf) is row (q & 3) + 8 (q >> 2) + 4 hf, column r: four runs
+// of four consecutive rows.  bias_frag: the accumulator holding b[row] in every column;
+// store_rows(_tanh): (tanh of) column r's 16 values into the LDS row `dst` (= stage[r] + 32 block).
+__device__ __forceinline__ F16 bias_frag(const float* b, int hf) {
+  F16 v;
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    const float4 x = *reinterpret_cast<const float4*>(b + 8 * qq + 4 * hf);
+    v[4 * qq] = x.x; v[4 * qq + 1] = x.y; v[4 * qq + 2] = x.z; v[4 * qq + 3] = x.w;
+  }
+  return v;
+}
+__device__ __forceinline__ void store_rows(float* dst, const F16& v, int hf) {
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq)
+    *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) = make_float4(v[4 * qq], v[4 * qq + 1], v[4 * qq + 2], v[4 * qq + 3]);
+}
+__device__ __forceinline__ void store_rows_tanh(float* dst, const F16& v, int hf) {
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq)
+    *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) =
+        make_float4(tanhf(v[4 * qq]), tanhf(v[4 * qq + 1]), tanhf(v[4 * qq + 2]), tanhf(v[4 * qq + 3]));
+}
+
 #ifndef FSL_WAVES
 #define FSL_WAVES 2  // and their registers (256 per lane)
 #endif
@@ -67,97 +95,98 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 template <int OUT>
 __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict__ rows, int64_t n, int64_t tiles,
-                                                 const float* __restrict__ w1, const float* __restrict__ b1,
-                                                 const float* __restrict__ w2, const float* __restrict__ b2,
-                                                 const float* __restrict__ w3, const float* __restrict__ b3,
-                                                 Coef c, float* __restrict__ partial) {
-  __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample
+                                                         const float* __restrict__ w1, const float* __restrict__ b1,
+                                                         const float* __restrict__ w2, const float* __restrict__ b2,
+                                                         const float* __restrict__ w3, const float* __restrict__ b3,
+                                                         Coef c, float* __restrict__ partial) {
+  __shared__ float sX[kTile][kF];
+  __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample, then g1
   __shared__ float sH2[kTile][kPad];  // rows: h2, then g2
   __shared__ float sG3[kTile][8];
-  __shared__ float sX[kTile][kF];
 
-  const int lane = threadIdx.x;
-  F2 dW2[kH / 2], dW1[kF / 2];  // lane i's rows, as pairs
-  float dW3[OUT], dB3[OUT];
-  float dB1 = 0.f, dB2 = 0.f, pg_sum = 0.f, vf_sum = 0.f, ent_sum = 0.f;
+  const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
+  F16 dW2[2][2];  // dW2 as four 32 x 32 MFMA accumulators [i block][k block]
+  float dW1[kF], dW3[OUT], dB3[OUT], dB2[2] = {0.f, 0.f};
+  float dB1 = 0.f, pg_sum = 0.f, vf_sum = 0.f, ent_sum = 0.f;
 #pragma unroll
-  for (int k = 0; k < kH / 2; ++k) dW2[k] = F2{0.f, 0.f};
+  for (int q = 0; q < 16; ++q) dW2[0][0][q] = dW2[0][1][q] = dW2[1][0][q] = dW2[1][1][q] = 0.f;
 #pragma unroll
-  for (int f = 0; f < kF / 2; ++f) dW1[f] = F2{0.f, 0.f};
+  for (int f = 0; f < kF; ++f) dW1[f] = 0.f;
 #pragma unroll
   for (int o = 0; o < OUT; ++o) dW3[o] = dB3[o] = 0.f;
-  const float b2j = b2[lane];
 
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    // W1, B1, W3, B3: wave-uniform scalar loads, opaque per tile (hoisted out of the loop they
-    // would not fit the SGPRs); the constant address space keeps them scalar loads
-    // (W2's row / column loads of phases 2 and 5 likewise: hoisted, they would hold 128 VGPRs
-    // across the whole loop)
-    const float *w1v = w1, *b1v = b1, *w2v = w2, *w3v = w3, *b3v = b3;
-    asm volatile("" : "+s"(w1v), "+s"(b1v), "+s"(w2v), "+s"(w3v), "+s"(b3v));
-    const CPtr W1 = (CPtr)w1v, B1 = (CPtr)b1v, W3 = (CPtr)w3v, B3 = (CPtr)b3v;
+    // weights re-read every tile (L1 / scalar-cache hits): hoisted out of the loop they would
+    // hold ~200 registers; W3 / B3 as wave-uniform scalar loads (constant address space)
+    const float *w1v = w1, *b1v = b1, *w2v = w2, *b2v = b2, *w3v = w3, *b3v = b3;
+    asm volatile("" : "+s"(w1v), "+s"(b1v), "+s"(w2v), "+s"(b2v), "+s"(w3v), "+s"(b3v));
+    const CPtr W3 = (CPtr)w3v, B3 = (CPtr)b3v;
     const int64_t left = n - tile * kTile;
     const int ns = (int)(left < kTile ? left : kTile);
-    const bool valid = lane < ns;
+    const bool valid = lane < ns;  // rows past n: x = 0 and g3 = 0, so they add nothing
 
-    // ---- phase 1 (lane = sample): x -> h1, staged as rows ------------------------------------
-    float x[kF], tail[4];
+    // ---- rows -> x (LDS) and the loss inputs (registers of lanes < kTile) --------------------
+    float tail[4] = {0.f, 0.f, 0.f, 0.f};
     if (lane < kTile) {
-      const float4* r = reinterpret_cast<const float4*>(rows + (tile * kTile + (valid ? lane : 0)) * kRow);
-      const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-      x[0] = r0.x; x[1] = r0.y; x[2] = r0.z; x[3] = r0.w;
-      x[4] = r1.x; x[5] = r1.y; x[6] = r1.z; x[7] = r1.w;
+      const float4* rp = reinterpret_cast<const float4*>(rows + (tile * kTile + (valid ? lane : 0)) * kRow);
+      float4 r0 = rp[0], r1 = rp[1];
+      const float4 r2 = rp[2];
+      if (!valid) r0 = r1 = make_float4(0.f, 0.f, 0.f, 0.f);
       tail[0] = r2.x; tail[1] = r2.y; tail[2] = r2.z; tail[3] = r2.w;
-#pragma unroll
-      for (int f = 0; f < kF; ++f) x[f] = valid ? x[f] : 0.f;
-#pragma unroll
-      for (int j = 0; j < kH; j += 4) {
-        float h[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float a = B1[j + q];
-#pragma unroll
-          for (int f = 0; f < kF; ++f) a = fmaf(W1[(j + q) * kF + f], x[f], a);
-          h[q] = tanhf(a);
-        }
-        *reinterpret_cast<float4*>(&sH1[lane][j]) = make_float4(h[0], h[1], h[2], h[3]);
-      }
-      *reinterpret_cast<float4*>(&sX[lane][0]) = make_float4(x[0], x[1], x[2], x[3]);
-      *reinterpret_cast<float4*>(&sX[lane][4]) = make_float4(x[4], x[5], x[6], x[7]);
+      *reinterpret_cast<float4*>(&sX[lane][0]) = r0;
+      *reinterpret_cast<float4*>(&sX[lane][4]) = r1;
     }
     __syncthreads();
 
-    // ---- phase 2 (lane = unit j): h2[s][j] = tanh(b2[j] + W2[j] . h1[s]), W2's row j in registers
-    // (packed f32 pairs: one v_pk_fma_f32 per two weights)
+    // ---- layer 1 on MFMA: H1^T[j][s] = b1[j] + sum_f W1[j][f] X[s][f]; K = 8 as 4 steps of
+    // (f = t, t + 4): lane (r, hf) supplies A = W1[32 jb + r][t + 4 hf], B = X[r][t + 4 hf] ----
     {
-      F2 w2r[kH / 2];
+      const float4 xb = *reinterpret_cast<const float4*>(&sX[r][4 * hf]);
 #pragma unroll
-      for (int k = 0; k < kH; k += 4) {
-        const float4 w = *reinterpret_cast<const float4*>(&w2v[lane * kH + k]);
-        w2r[k / 2] = F2{w.x, w.y};
-        w2r[k / 2 + 1] = F2{w.z, w.w};
-      }
-      for (int t = 0; t < ns; ++t) {
-        F2 acc[4] = {F2{b2j, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}};  // 8 partial sums
-#pragma unroll
-        for (int k = 0; k < kH; k += 4) {
-          const float4 h = *reinterpret_cast<const float4*>(&sH1[t][k]);
-          acc[(k / 4) & 1] = fma2(w2r[k / 2], F2{h.x, h.y}, acc[(k / 4) & 1]);
-          acc[2 + ((k / 4) & 1)] = fma2(w2r[k / 2 + 1], F2{h.z, h.w}, acc[2 + ((k / 4) & 1)]);
-        }
-        const F2 a = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-        sH2[t][lane] = tanhf(a.x + a.y);
+      for (int jb = 0; jb < 2; ++jb) {
+        const float4 wa = *reinterpret_cast<const float4*>(&w1v[(32 * jb + r) * kF + 4 * hf]);
+        F16 acc = bias_frag(b1v + 32 * jb, hf);
+        acc = mfma32(wa.x, xb.x, acc);
+        acc = mfma32(wa.y, xb.y, acc);
+        acc = mfma32(wa.z, xb.z, acc);
+        acc = mfma32(wa.w, xb.w, acc);
+        store_rows_tanh(&sH1[r][32 * jb], acc, hf);
       }
     }
     __syncthreads();
 
-    // ---- phase 3 (lane = sample): the output, the loss gradient g3 and g2 = (W3^T g3)(1 - h2^2)
+    // ---- layer 2 on MFMA: H2^T[j][s] = b2[j] + sum_k W2[j][k] H1[s][k]; K = 64 as 32 steps of
+    // (k = t, t + 32): A = W2[32 jb + r][t + 32 hf] (row loads), B = H1[r][t + 32 hf] (LDS row) ----
+    {
+      float hb[32];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(&sH1[r][32 * hf + 4 * u]);
+        hb[4 * u] = v.x; hb[4 * u + 1] = v.y; hb[4 * u + 2] = v.z; hb[4 * u + 3] = v.w;
+      }
+#pragma unroll 1
+      for (int jb = 0; jb < 2; ++jb) {  // (one block's weights live at a time)
+        float wa[32];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float4 v = *reinterpret_cast<const float4*>(&w2v[(32 * jb + r) * kH + 32 * hf + 4 * u]);
+          wa[4 * u] = v.x; wa[4 * u + 1] = v.y; wa[4 * u + 2] = v.z; wa[4 * u + 3] = v.w;
+        }
+        F16 acc = bias_frag(b2v + 32 * jb, hf);
+#pragma unroll
+        for (int t = 0; t < 32; ++t) acc = mfma32(wa[t], hb[t], acc);
+        store_rows_tanh(&sH2[r][32 * jb], acc, hf);
+      }
+    }
+    __syncthreads();
+
+    // ---- (lane = sample) the output, the loss gradient g3 and g2 = (W3^T g3)(1 - h2^2) ---------
     float g2[kH];
     if (lane < kTile) {
 #pragma unroll
       for (int k = 0; k < kH; k += 4) {
-        const float4 h = *reinterpret_cast<const float4*>(&sH2[lane][k]);
-        g2[k] = h.x; g2[k + 1] = h.y; g2[k + 2] = h.z; g2[k + 3] = h.w;  // h2 for now
+        const float4 v = *reinterpret_cast<const float4*>(&sH2[lane][k]);
+        g2[k] = v.x; g2[k + 1] = v.y; g2[k + 2] = v.z; g2[k + 3] = v.w;  // h2 for now
       }
       float g3[8];
       if constexpr (OUT == 8) {
@@ -188,13 +217,13 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
           ent -= p[o] * lp[o];
         }
         const float adv = tail[2];
-        const float r = expf(lp_a - tail[1]);
-        const float s1 = r * adv, rc = fminf(fmaxf(r, 1.f - c.clip), 1.f + c.clip), s2 = rc * adv;
+        const float rt = expf(lp_a - tail[1]);
+        const float s1 = rt * adv, rc = fminf(fmaxf(rt, 1.f - c.clip), 1.f + c.clip), s2 = rc * adv;
         // torch.min's gradient goes to the smaller operand (half to each on a tie); clamp's passes
         // inside [1 - clip, 1 + clip]
-        const float inr = (r >= 1.f - c.clip && r <= 1.f + c.clip) ? 1.f : 0.f;
+        const float inr = (rt >= 1.f - c.clip && rt <= 1.f + c.clip) ? 1.f : 0.f;
         const float wsel = s1 < s2 ? 1.f : (s1 > s2 ? inr : 0.5f + 0.5f * inr);
-        const float g_lpa = -(adv * wsel) * c.inv_n * r;
+        const float g_lpa = -(adv * wsel) * c.inv_n * rt;
         const float g_ent = c.ent_coef * c.inv_n;  // d(-ent_coef mean H) / d(exp(lp) lp) per term
         float g_lp[8], gsum = 0.f;
 #pragma unroll
@@ -230,7 +259,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     }
     __syncthreads();
 
-    // ---- phase 4 (lane = unit j): dW3's column j from h2's column and g3's rows ----------------
+    // ---- (lane = unit j) dW3's column j from h2's column and g3's rows -------------------------
     for (int t = 0; t < ns; ++t) {
       const float h2c = sH2[t][lane];
 #pragma unroll
@@ -244,37 +273,66 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     }
     __syncthreads();
 
-    // ---- phase 5 (lane = unit i): g1 = (W2^T g2)(1 - h1^2), dW2 / dW1 rows, db1 / db2 -----------
+    // ---- dW2[i][k] += sum_s G2[s][i] H1[s][k] on MFMA: K = the tile's samples as 16 steps of
+    // (s = t, t + 16): A = G2[t + 16 hf][32 ib + r], B = H1[t + 16 hf][32 kb + r]; db2 alongside ---
+#pragma unroll
+    for (int t = 0; t < kTile / 2; ++t) {
+      const int sidx = t + (kTile / 2) * hf;
+      const float a0 = sH2[sidx][r], a1 = sH2[sidx][32 + r];
+      const float h0 = sH1[sidx][r], h1v = sH1[sidx][32 + r];
+      dB2[0] += a0;
+      dB2[1] += a1;
+      dW2[0][0] = mfma32(a0, h0, dW2[0][0]);
+      dW2[0][1] = mfma32(a0, h1v, dW2[0][1]);
+      dW2[1][0] = mfma32(a1, h0, dW2[1][0]);
+      dW2[1][1] = mfma32(a1, h1v, dW2[1][1]);
+    }
+    __syncthreads();
+
+    // ---- backward through W2 on MFMA: gh1^T[i][s] = sum_j W2[j][i] G2[s][j] (A = W2[t + 32 hf][32 ib
+    // + r], B = G2[r][t + 32 hf]); g1 = gh1 (1 - h1^2) overwrites h1 where this lane read it ---------
     {
-      F2 w2c[kH / 2];
+      float gb[32];
 #pragma unroll
-      for (int j = 0; j < kH; j += 2) w2c[j / 2] = F2{w2v[j * kH + lane], w2v[(j + 1) * kH + lane]};
-      for (int t = 0; t < ns; ++t) {
-        const float g2c = sH2[t][lane];
-        const F2 g2s = F2{g2c, g2c};
-        dB2 += g2c;
-        F2 gh[4] = {F2{0.f, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}, F2{0.f, 0.f}};
-#pragma unroll
-        for (int j = 0; j < kH; j += 4) {
-          const float4 g = *reinterpret_cast<const float4*>(&sH2[t][j]);
-          const float4 h = *reinterpret_cast<const float4*>(&sH1[t][j]);
-          gh[(j / 4) & 1] = fma2(w2c[j / 2], F2{g.x, g.y}, gh[(j / 4) & 1]);
-          gh[2 + ((j / 4) & 1)] = fma2(w2c[j / 2 + 1], F2{g.z, g.w}, gh[2 + ((j / 4) & 1)]);
-          dW2[j / 2] = fma2(g2s, F2{h.x, h.y}, dW2[j / 2]);
-          dW2[j / 2 + 1] = fma2(g2s, F2{h.z, h.w}, dW2[j / 2 + 1]);
-        }
-        const F2 ga = (gh[0] + gh[1]) + (gh[2] + gh[3]);
-        const float h1c = sH1[t][lane];
-        const float g1 = (ga.x + ga.y) * (1.f - h1c * h1c);
-        dB1 += g1;
-        const float4 xa = *reinterpret_cast<const float4*>(&sX[t][0]);
-        const float4 xb = *reinterpret_cast<const float4*>(&sX[t][4]);
-        const F2 g1s = F2{g1, g1};
-        dW1[0] = fma2(g1s, F2{xa.x, xa.y}, dW1[0]);
-        dW1[1] = fma2(g1s, F2{xa.z, xa.w}, dW1[1]);
-        dW1[2] = fma2(g1s, F2{xb.x, xb.y}, dW1[2]);
-        dW1[3] = fma2(g1s, F2{xb.z, xb.w}, dW1[3]);
+      for (int u = 0; u < 8; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(&sH2[r][32 * hf + 4 * u]);
+        gb[4 * u] = v.x; gb[4 * u + 1] = v.y; gb[4 * u + 2] = v.z; gb[4 * u + 3] = v.w;
       }
+#pragma unroll 1
+      for (int ib = 0; ib < 2; ++ib) {
+        float wa[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) wa[t] = w2v[(t + 32 * hf) * kH + 32 * ib + r];
+        F16 acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 32; ++t) acc = mfma32(wa[t], gb[t], acc);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {  // rows i = 32 ib + 8 qq + 4 hf + (0..3) of sample r
+          float4* hp = reinterpret_cast<float4*>(&sH1[r][32 * ib + 8 * qq + 4 * hf]);
+          const float4 hv = *hp;
+          *hp = make_float4(acc[4 * qq] * (1.f - hv.x * hv.x), acc[4 * qq + 1] * (1.f - hv.y * hv.y),
+                            acc[4 * qq + 2] * (1.f - hv.z * hv.z), acc[4 * qq + 3] * (1.f - hv.w * hv.w));
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- (lane = unit i) dW1's row i and db1 from g1's column and x's rows ---------------------
+    for (int t = 0; t < ns; ++t) {
+      const float g = sH1[t][lane];
+      dB1 += g;
+      const float4 xa = *reinterpret_cast<const float4*>(&sX[t][0]);
+      const float4 xb = *reinterpret_cast<const float4*>(&sX[t][4]);
+      dW1[0] = fmaf(g, xa.x, dW1[0]);
+      dW1[1] = fmaf(g, xa.y, dW1[1]);
+      dW1[2] = fmaf(g, xa.z, dW1[2]);
+      dW1[3] = fmaf(g, xa.w, dW1[3]);
+      dW1[4] = fmaf(g, xb.x, dW1[4]);
+      dW1[5] = fmaf(g, xb.y, dW1[5]);
+      dW1[6] = fmaf(g, xb.z, dW1[6]);
+      dW1[7] = fmaf(g, xb.w, dW1[7]);
     }
     __syncthreads();  // the next tile's stage overwrites what this one read
   }
@@ -282,11 +340,22 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
   // ---- this wave's partial gradient --------------------------------------------------------
   float* out = partial + (size_t)blockIdx.x * partial_stride<OUT>();
 #pragma unroll
-  for (int f = 0; f < kF; ++f) out[lane * kF + f] = dW1[f / 2][f & 1];
+  for (int f = 0; f < kF; ++f) out[lane * kF + f] = dW1[f];
   out[kOffB1 + lane] = dB1;
 #pragma unroll
-  for (int k = 0; k < kH; ++k) out[kOffW2 + lane * kH + k] = dW2[k / 2][k & 1];
-  out[kOffB2 + lane] = dB2;
+  for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = 32 * ib + (q & 3) + 8 * (q >> 2) + 4 * hf;  // the accumulator's row map
+        out[kOffW2 + i * kH + 32 * kb + r] = dW2[ib][kb][q];
+      }
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib) {
+    const float d = dB2[ib] + __shfl_xor(dB2[ib], 32, 64);  // the two sample halves
+    if (hf == 0) out[kOffB2 + 32 * ib + r] = d;
+  }
 #pragma unroll
   for (int o = 0; o < OUT; ++o) out[kOffW3 + o * kH + lane] = dW3[o];
 #pragma unroll
