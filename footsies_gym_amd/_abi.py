@@ -147,6 +147,8 @@ LIB_FUNCTIONS = {
     "fs_step_n": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(fs_outputs)]),
     "fs_step_n_policy": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(fs_policy), C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_ppo_workspace_bytes": (C.c_size_t, []),
+    "fs_ppo_eval": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp),
+                              C.c_void_p, C.c_void_p, C.c_void_p]),
     "fs_ppo_grad": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp), C.c_float, C.c_float,
                               C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "fs_hash_actions": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),

@@ -509,6 +509,28 @@ FS_API int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const 
   return FS_OK;
 }
 
+FS_API int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp, const fs_mlp* actor,
+                       const fs_mlp* critic, float* values_out, float* logp_out, void* stream) {
+  if (!x || n_values <= 0 || n_logp < 0 || n_logp > n_values)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: x, n_values > 0 and 0 <= n_logp <= n_values required");
+  if (reinterpret_cast<uintptr_t>(x) % 16) return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: x must be 16-byte aligned");
+  if (values_out && !critic) return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: values_out needs the critic");
+  if (logp_out && n_logp > 0 && (!actor || !actions))
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: logp_out needs the actor and actions");
+  const fs_mlp none{};
+  const fs_mlp& A = actor ? *actor : none;
+  const fs_mlp& Cn = critic ? *critic : none;
+  const float* const a[6] = {A.w1, A.b1, A.w2, A.b2, A.w3, A.b3};
+  const float* const c[6] = {Cn.w1, Cn.b1, Cn.w2, Cn.b2, Cn.w3, Cn.b3};
+  for (int i = 0; i < 6; ++i)
+    if ((values_out && !c[i]) || (logp_out && n_logp > 0 && !a[i]))
+      return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: all six arrays of each network used required");
+  const hipError_t e = fsk::launch_ppo_eval(x, n_values, actions, n_logp, a, c, values_out, logp_out,
+                                            static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_eval: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
 FS_API int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out) {
   if (!h || !p1_out || n_steps <= 0) return FS_E_INVALID;
   int rc;

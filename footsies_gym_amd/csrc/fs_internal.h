@@ -133,5 +133,8 @@ size_t ppo_workspace_bytes();
 hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
                            float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
                            hipStream_t s);
+hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp,
+                           const float* const actor[6], const float* const critic[6], float* values, float* logp,
+                           hipStream_t s);
 
 }  // namespace fsk

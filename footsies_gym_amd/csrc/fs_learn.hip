@@ -93,12 +93,16 @@ __device__ __forceinline__ void store_rows_tanh(float* dst, const F16& v, int hf
 #define FSL_OCC
 #endif
 
-template <int OUT>
+// EVAL: the forward pass only (fs_ppo_eval), rows = x [n][8]; the critic writes v per row into
+// out, the actor log_softmax(logits)[actions[row]].  Otherwise the gradient, rows [n][12].
+template <int OUT, bool EVAL = false>
 __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict__ rows, int64_t n, int64_t tiles,
                                                          const float* __restrict__ w1, const float* __restrict__ b1,
                                                          const float* __restrict__ w2, const float* __restrict__ b2,
                                                          const float* __restrict__ w3, const float* __restrict__ b3,
-                                                         Coef c, float* __restrict__ partial) {
+                                                         Coef c, float* __restrict__ partial,
+                                                         const uint8_t* __restrict__ actions = nullptr) {
+  constexpr int kStride = EVAL ? kF : kRow;
   __shared__ float sX[kTile][kF];
   __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample, then g1
   __shared__ float sH2[kTile][kPad];  // rows: h2, then g2
@@ -128,11 +132,13 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     // ---- rows -> x (LDS) and the loss inputs (registers of lanes < kTile) --------------------
     float tail[4] = {0.f, 0.f, 0.f, 0.f};
     if (lane < kTile) {
-      const float4* rp = reinterpret_cast<const float4*>(rows + (tile * kTile + (valid ? lane : 0)) * kRow);
+      const float4* rp = reinterpret_cast<const float4*>(rows + (tile * kTile + (valid ? lane : 0)) * kStride);
       float4 r0 = rp[0], r1 = rp[1];
-      const float4 r2 = rp[2];
+      if constexpr (!EVAL) {
+        const float4 r2 = rp[2];
+        tail[0] = r2.x; tail[1] = r2.y; tail[2] = r2.z; tail[3] = r2.w;
+      }
       if (!valid) r0 = r1 = make_float4(0.f, 0.f, 0.f, 0.f);
-      tail[0] = r2.x; tail[1] = r2.y; tail[2] = r2.z; tail[3] = r2.w;
       *reinterpret_cast<float4*>(&sX[lane][0]) = r0;
       *reinterpret_cast<float4*>(&sX[lane][4]) = r1;
     }
@@ -179,6 +185,46 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       }
     }
     __syncthreads();
+
+    if constexpr (EVAL) {  // (lane = sample) the output only
+      if (valid) {
+        float hv[kH];
+#pragma unroll
+        for (int k = 0; k < kH; k += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(&sH2[lane][k]);
+          hv[k] = v.x; hv[k + 1] = v.y; hv[k + 2] = v.z; hv[k + 3] = v.w;
+        }
+        const int64_t srow = tile * kTile + lane;
+        if constexpr (OUT == 8) {
+          float z[8];
+#pragma unroll
+          for (int o = 0; o < 8; ++o) {
+            float a = B3[o];
+#pragma unroll
+            for (int j = 0; j < kH; ++j) a = fmaf(W3[o * kH + j], hv[j], a);
+            z[o] = a;
+          }
+          float m = z[0];
+#pragma unroll
+          for (int o = 1; o < 8; ++o) m = fmaxf(m, z[o]);
+          float se = 0.f;
+#pragma unroll
+          for (int o = 0; o < 8; ++o) se += expf(z[o] - m);
+          const int act = actions[srow];
+          float za = z[0];
+#pragma unroll
+          for (int o = 1; o < 8; ++o) za = o == act ? z[o] : za;
+          partial[srow] = za - (m + logf(se));
+        } else {
+          float v = B3[0];
+#pragma unroll
+          for (int j = 0; j < kH; ++j) v = fmaf(W3[j], hv[j], v);
+          partial[srow] = v;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
 
     // ---- (lane = sample) the output, the loss gradient g3 and g2 = (W3^T g3)(1 - h2^2) ---------
     float g2[kH];
@@ -337,6 +383,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     __syncthreads();  // the next tile's stage overwrites what this one read
   }
 
+  if constexpr (EVAL) return;
   // ---- this wave's partial gradient --------------------------------------------------------
   float* out = partial + (size_t)blockIdx.x * partial_stride<OUT>();
 #pragma unroll
@@ -423,6 +470,26 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
                      c.inv_n);
   hipLaunchKernelGGL(k_ppo_reduce<1>, dim3((n_params<1>() + 3 + 63) / 64), dim3(1024), 0, s, pc, waves,
                      grad + n_params<8>(), loss, c.inv_n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp,
+                           const float* const actor[6], const float* const critic[6], float* values, float* logp,
+                           hipStream_t s) {
+  using namespace fsl;
+  const Coef c{0.f, 0.f, 0.f, 0.f};
+  if (values && n_values > 0) {
+    const int64_t tiles = (n_values + kTile - 1) / kTile;
+    const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
+    hipLaunchKernelGGL((k_ppo_grad<1, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, critic[0], critic[1],
+                       critic[2], critic[3], critic[4], critic[5], c, values, nullptr);
+  }
+  if (logp && n_logp > 0) {
+    const int64_t tiles = (n_logp + kTile - 1) / kTile;
+    const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
+    hipLaunchKernelGGL((k_ppo_grad<8, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, actor[0], actor[1],
+                       actor[2], actor[3], actor[4], actor[5], c, logp, actions);
+  }
   return hipGetLastError();
 }
 

@@ -139,6 +139,25 @@ class PPOGrad:
         self._mlps = [_abi.fs_mlp(*[t.data_ptr() for t in params]) for params in nets]
         self.device = dev
 
+    def evaluate(self, x, actions=None, n_logp=0):
+        """fs_ppo_eval: (critic(x) [n], log_softmax(actor(x[:n_logp]))[actions] [n_logp] or None),
+        fp32, without gradient; x: device [n, 8] fp32, actions: device uint8 [n_logp]."""
+        torch = _torch()
+        if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES or not x.is_contiguous():
+            raise ValueError("x must be a contiguous [n, 8] float32 tensor")
+        n = x.shape[0]
+        values = torch.empty(n, dtype=torch.float32, device=x.device)
+        logp = None
+        if n_logp:
+            if actions is None or actions.dtype != torch.uint8 or actions.numel() < n_logp or not actions.is_contiguous():
+                raise ValueError("actions must be a contiguous uint8 tensor of at least n_logp entries")
+            logp = torch.empty(n_logp, dtype=torch.float32, device=x.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().fs_ppo_eval(C.c_void_p(x.data_ptr()), n, C.c_void_p(actions.data_ptr() if n_logp else None),
+                                n_logp, C.byref(self._mlps[0]), C.byref(self._mlps[1]), C.c_void_p(values.data_ptr()),
+                                C.c_void_p(logp.data_ptr() if n_logp else None), C.c_void_p(stream)))
+        return values, logp
+
     def __call__(self, rows, clip, vf_coef, ent_coef):
         """rows: device [n][12] fp32 (features, action, old log-prob, advantage, return)."""
         torch = _torch()
@@ -219,11 +238,15 @@ class PPOTrainer:
         torch = _torch()
         T, N = actions.shape
         with torch.no_grad():
-            values = self.critic(feats).squeeze(-1)  # [T+1][N]
-            adv, ret = gae(rewards, values, dones, self.gamma, self.lam)
             x = feats[:T].reshape(T * N, N_FEATURES)
             a = actions.reshape(T * N)
-            old32 = torch.log_softmax(self.actor(x), dim=1).gather(1, a[:, None])[:, 0]
+            if self._grad is not None:  # both forward passes in two fused launches
+                v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), self.actions.view(-1), T * N)
+                values = v.view(T + 1, N)
+            else:
+                values = self.critic(feats).squeeze(-1)  # [T+1][N]
+                old32 = torch.log_softmax(self.actor(x), dim=1).gather(1, a[:, None])[:, 0]
+            adv, ret = gae(rewards, values, dones, self.gamma, self.lam)
             behav = self.logp.reshape(T * N)  # what the kernel sampled with (bf16 actor)
             gap = behav - old32
             old = behav if self.old_logp == "behaviour" else old32

@@ -297,6 +297,12 @@ size_t fs_ppo_workspace_bytes(void);
  * splits a tie's gradient, clamp passes it inside its closed range); loss_out: device
  * [3] f32 = the three means (policy, value, entropy).  Summation order is fixed, so
  * repeated calls give identical results. */
+/* The update's forward passes without gradient, fp32, asynchronously on `stream`: for
+ * x = device [n_values][8] f32 features, values_out[i] = critic(x[i]) for i < n_values, and
+ * logp_out[i] = log_softmax(actor(x[i]))[actions[i]] for i < n_logp <= n_values (actions:
+ * device uint8 [n_logp]).  Either output may be NULL (its network is then not run). */
+int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp, const fs_mlp* actor,
+                const fs_mlp* critic, float* values_out, float* logp_out, void* stream);
 int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
                 float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
                 size_t workspace_bytes, void* stream);

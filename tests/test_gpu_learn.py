@@ -132,3 +132,23 @@ def test_ppo_trainer_hip_step_equals_torch_step():
         flips += int((d > 1e-6).sum())
     total = sum(p.numel() for p in res[0])
     assert flips <= total // 1000, (flips, total)
+
+
+@pytest.mark.parametrize("n,n_logp", [(1, 1), (100, 37), (70001, 70001), (131072 + 65536, 131072)])
+def test_ppo_eval_matches_torch_forward(n, n_logp):
+    """fs_ppo_eval: critic values of every row and the actor's log-probability of the taken action
+    for the first n_logp rows, against the torch modules' forward pass (fp32, same tolerance)."""
+    import torch
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=3)
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x = (torch.rand((n, 8), generator=g, device="cuda") * 2 - 0.5).contiguous()
+    a = torch.randint(0, 8, (n_logp,), generator=g, device="cuda").to(torch.uint8)
+    v, lp = PPOGrad(actor, critic).evaluate(x, a, n_logp)
+    with torch.no_grad():
+        v_ref = critic(x).squeeze(-1)
+        lp_ref = torch.log_softmax(actor(x[:n_logp]), 1).gather(1, a.long()[:, None])[:, 0]
+    torch.testing.assert_close(v, v_ref, rtol=RTOL, atol=1e-5)
+    torch.testing.assert_close(lp, lp_ref, rtol=RTOL, atol=1e-5)
+    v2, lp2 = PPOGrad(actor, critic).evaluate(x)
+    assert lp2 is None and torch.equal(v2, v)
