@@ -289,8 +289,9 @@ def issue_profile(kernel, envs, ticks):
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))):
         with open(path) as f:
             doc = json.load(f)
-        for k in doc.get("kernels", []):
-            if k["kernel"] == kernel and k["envs"] == envs:
+        kernels = doc.get("kernels", []) if isinstance(doc, dict) else []
+        for k in kernels if isinstance(kernels, list) else []:  # (other summaries have other layouts)
+            if isinstance(k, dict) and k.get("kernel") == kernel and k.get("envs") == envs:
                 pw = k["per_wave_tick"]
                 best = {"bound": "each wave's own instruction issue (one instruction per wave per 4 cycles, "
                                  "MI355X_MICROARCH.md constants table) and its exposed LDS waits (DESIGN.md section 5)",
