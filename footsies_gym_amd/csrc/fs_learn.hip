@@ -60,6 +60,22 @@ typedef float F16 __attribute__((ext_vector_type(16)));  // a 32 x 32 f32 MFMA a
 __device__ __forceinline__ F16 mfma32(float a, float b, F16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
+// tanh without branches (the library tanhf runs both of its branches under divergence, ~30
+// instructions): |x| < 0.625 the same odd polynomial, above it 1 - 2 / (2^(2|x| log2 e) + 1)
+// with the hardware exp2 and reciprocal (within a few ulp of tanhf; 2^+inf -> 1 exactly).
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float ax = fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);
+  const float big = fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+  const float x2 = x * x;
+  float p = fmaf(-0.005700020585209131f, x2, 0.02063407190144062f);  // 0xbbbac73d, 0x3ca908c9
+  p = fmaf(x2, p, -0.053737930953502655f);                            // 0xbd5c1c4e
+  p = fmaf(x2, p, 0.13331416249275208f);                              // 0x3e088382
+  p = fmaf(x2, p, -0.3333328068256378f);                              // 0xbeaaaa99
+  const float small = fmaf(x2, ax * p, ax);
+  return copysignf(ax < 0.625f ? small : big, x);
+}
+
 // Accumulator element q of lane (r, hf) is row (q & 3) + 8 (q >> 2) + 4 hf, column r: four runs
 // of four consecutive rows.  bias_frag: the accumulator holding b[row] in every column;
 // store_rows(_tanh): (tanh of) column r's 16 values into the LDS row `dst` (= stage[r] + 32 block).
@@ -81,7 +97,7 @@ __device__ __forceinline__ void store_rows_tanh(float* dst, const F16& v, int hf
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq)
     *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) =
-        make_float4(tanhf(v[4 * qq]), tanhf(v[4 * qq + 1]), tanhf(v[4 * qq + 2]), tanhf(v[4 * qq + 3]));
+        make_float4(tanh_fast(v[4 * qq]), tanh_fast(v[4 * qq + 1]), tanh_fast(v[4 * qq + 2]), tanh_fast(v[4 * qq + 3]));
 }
 
 #ifndef FSL_WAVES
