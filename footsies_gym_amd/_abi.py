@@ -151,6 +151,10 @@ LIB_FUNCTIONS = {
                               C.c_void_p, C.c_void_p, C.c_void_p]),
     "fs_ppo_grad": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp), C.c_float, C.c_float,
                               C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "fs_ppo_gae": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_float,
+                             C.c_void_p, C.c_void_p, C.c_void_p]),
+    "fs_ppo_pack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                              C.c_void_p, C.c_void_p]),
     "fs_hash_actions": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "fs_outputs_get": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_pack_outputs": (C.c_int, [C.c_void_p, C.c_void_p]),

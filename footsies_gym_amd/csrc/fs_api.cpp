@@ -531,6 +531,28 @@ FS_API int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions,
   return FS_OK;
 }
 
+FS_API int fs_ppo_gae(const double* rewards, const uint8_t* done, const float* values, int T, int64_t N, float gamma,
+                      float gamma_lam, float* adv_out, float* ret_out, void* stream) {
+  if (!rewards || !done || !values || !adv_out || !ret_out || T <= 0 || N <= 0)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_gae: all five arrays, T > 0 and N > 0 required");
+  const hipError_t e = fsk::launch_ppo_gae(rewards, done, values, T, N, gamma, gamma_lam, adv_out, ret_out,
+                                           static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_gae: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
+FS_API int fs_ppo_pack(const float* x, const uint8_t* actions, const float* old_logp, const float* adv,
+                       const float* ret, const float* stats, int64_t n, float* rows_out, void* stream) {
+  if (!x || !actions || !old_logp || !adv || !ret || !stats || !rows_out || n <= 0)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_pack: all seven arrays and n > 0 required");
+  if (reinterpret_cast<uintptr_t>(x) % 16 || reinterpret_cast<uintptr_t>(rows_out) % 16)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_pack: x and rows_out must be 16-byte aligned");
+  const hipError_t e = fsk::launch_ppo_pack(x, actions, old_logp, adv, ret, stats, n, rows_out,
+                                            static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_pack: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
 FS_API int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_t* p1_out, uint8_t* p2_out) {
   if (!h || !p1_out || n_steps <= 0) return FS_E_INVALID;
   int rc;

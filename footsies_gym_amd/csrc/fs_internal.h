@@ -136,5 +136,9 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
 hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp,
                            const float* const actor[6], const float* const critic[6], float* values, float* logp,
                            hipStream_t s);
+hipError_t launch_ppo_gae(const double* rew, const uint8_t* done, const float* val, int T, int64_t N, float gamma,
+                          float gamma_lam, float* adv, float* ret, hipStream_t s);
+hipError_t launch_ppo_pack(const float* x, const uint8_t* act, const float* old, const float* adv, const float* ret,
+                           const float* stats, int64_t n, float* rows, hipStream_t s);
 
 }  // namespace fsk

@@ -459,9 +459,61 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
   }
 }
 
+// GAE over a [T][N] trajectory (ppo.py gae): one lane per arena walks its ticks backwards, every
+// load coalesced across the wave's arenas.  The TD error keeps gae()'s op order, one rounding
+// per op (r + (gamma v[t+1]) keep) - v[t]; the recursion is addcmul's fused multiply-add.
+// Rewards (f64) and done flags (u8) are read as the trajectory holds them.
+__global__ __launch_bounds__(256) void k_ppo_gae(const double* __restrict__ rew, const uint8_t* __restrict__ done,
+                                                 const float* __restrict__ val, int T, int64_t N, float gamma,
+                                                 float gamma_lam, float* __restrict__ adv, float* __restrict__ ret) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f;
+#pragma unroll 4
+  for (int t = T - 1; t >= 0; --t) {
+    const int64_t i = (int64_t)t * N + n;
+    const float keep = 1.f - (float)done[i];
+    const float v0 = val[i];
+    const float delta = ((float)rew[i] + (gamma * val[i + N]) * keep) - v0;
+    a = t == T - 1 ? delta : fmaf(gamma_lam * keep, a, delta);
+    adv[i] = a;
+    ret[i] = a + v0;
+  }
+}
+
+// The update's sample table, one row per sample: x[8], action, old log-prob, the advantage
+// normalised as (adv - mean) / (std + 1e-8) with the batch statistics in stats[2], return.
+__global__ __launch_bounds__(256) void k_ppo_pack(const float* __restrict__ x, const uint8_t* __restrict__ act,
+                                                  const float* __restrict__ old, const float* __restrict__ adv,
+                                                  const float* __restrict__ ret, const float* __restrict__ stats,
+                                                  int64_t n, float* __restrict__ rows) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  const float4* xs = reinterpret_cast<const float4*>(x + m * kF);
+  float4* out = reinterpret_cast<float4*>(rows + m * kRow);
+  const float mean = stats[0], den = stats[1] + 1e-8f;
+  out[0] = xs[0];
+  out[1] = xs[1];
+  out[2] = make_float4((float)act[m], old[m], (adv[m] - mean) / den, ret[m]);
+}
+
 }  // namespace fsl
 
 namespace fsk {
+
+hipError_t launch_ppo_gae(const double* rew, const uint8_t* done, const float* val, int T, int64_t N, float gamma,
+                          float gamma_lam, float* adv, float* ret, hipStream_t s) {
+  hipLaunchKernelGGL(fsl::k_ppo_gae, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rew, done, val, T, N, gamma,
+                     gamma_lam, adv, ret);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_pack(const float* x, const uint8_t* act, const float* old, const float* adv, const float* ret,
+                           const float* stats, int64_t n, float* rows, hipStream_t s) {
+  hipLaunchKernelGGL(fsl::k_ppo_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, act, old, adv, ret,
+                     stats, n, rows);
+  return hipGetLastError();
+}
 
 size_t ppo_workspace_bytes() {
   return sizeof(float) * (size_t)fsl::kMaxWaves * (fsl::partial_stride<8>() + fsl::partial_stride<1>());

@@ -186,12 +186,52 @@ def gae(rewards, values, dones, gamma, lam):
     return adv, adv + values[:-1]
 
 
+def gae_device(rewards, dones, values, gamma, lam):
+    """gae() in one launch (fs_ppo_gae): rewards [T][N] f64 and dones [T][N] u8 as the trajectory
+    holds them, values [T + 1][N] f32; the TD errors in gae()'s op order, the recursion as a fused
+    multiply-add (addcmul's), so the two agree to fp32 rounding of that step."""
+    torch = _torch()
+    T, N = rewards.shape
+    if (rewards.dtype != torch.float64 or dones.dtype != torch.uint8 or values.dtype != torch.float32
+            or tuple(dones.shape) != (T, N) or tuple(values.shape) != (T + 1, N)
+            or not all(t.is_contiguous() for t in (rewards, dones, values))):
+        raise ValueError("gae_device: contiguous rewards f64 [T][N], dones u8 [T][N], values f32 [T+1][N]")
+    adv = torch.empty((T, N), dtype=torch.float32, device=values.device)
+    ret = torch.empty_like(adv)
+    g = torch.tensor([gamma, gamma * lam], dtype=torch.float32)  # the f32 scalars torch's ops use
+    stream = torch.cuda.current_stream(values.device).cuda_stream
+    check(lib().fs_ppo_gae(C.c_void_p(rewards.data_ptr()), C.c_void_p(dones.data_ptr()), C.c_void_p(values.data_ptr()),
+                           T, N, float(g[0]), float(g[1]), C.c_void_p(adv.data_ptr()), C.c_void_p(ret.data_ptr()),
+                           C.c_void_p(stream)))
+    return adv, ret
+
+
+def pack_rows(x, actions, old, adv, ret, out=None):
+    """fs_ppo_grad's [M, 12] sample table in one launch (fs_ppo_pack): x [M, 8] f32, actions u8
+    [M], old log-probs, advantages and returns f32 [M]; the advantages normalised on the way as
+    (adv - mean) / (std + 1e-8) with torch's mean and (unbiased) std."""
+    torch = _torch()
+    M = x.shape[0]
+    if (x.dtype != torch.float32 or tuple(x.shape) != (M, N_FEATURES) or actions.dtype != torch.uint8
+            or not all(t.is_contiguous() and t.numel() == M for t in (actions, old, adv, ret))
+            or not x.is_contiguous()):
+        raise ValueError("pack_rows: contiguous x f32 [M, 8], actions u8 [M], old / adv / ret f32 [M]")
+    stats = torch.stack([adv.mean(), adv.std()])
+    rows = out if out is not None else torch.empty((M, 12), dtype=torch.float32, device=x.device)
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    check(lib().fs_ppo_pack(C.c_void_p(x.data_ptr()), C.c_void_p(actions.data_ptr()), C.c_void_p(old.data_ptr()),
+                            C.c_void_p(adv.data_ptr()), C.c_void_p(ret.data_ptr()), C.c_void_p(stats.data_ptr()), M,
+                            C.c_void_p(rows.data_ptr()), C.c_void_p(stream)))
+    return rows
+
+
 class PPOTrainer:
     """PPO over a FootsiesSim (P2 = whatever the sim was created with).  `horizon` ticks per
     rollout, all arenas in every minibatch round."""
 
     def __init__(self, sim, actor=None, critic=None, horizon=128, gamma=0.99, lam=0.95, epochs=2, minibatches=4,
-                 lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour", learner="hip"):
+                 lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour", learner="hip",
+                 kl_ticks=None):
         torch = _torch()
         if old_logp not in ("behaviour", "fp32"):
             raise ValueError("old_logp must be 'behaviour' or 'fp32'")
@@ -205,6 +245,9 @@ class PPOTrainer:
         self.critic = critic if critic is not None else make_critic(device=dev, seed=seed + 1)
         self.rollout = FusedPolicyRollout(sim, self.actor, seed=seed)
         self.horizon, self.gamma, self.lam = horizon, gamma, lam
+        # the fp32 log-probs behind kl_behaviour_fp32 / logp_abs_diff: every tick when they are
+        # PPO's old log-probs, else a sample of the first `kl_ticks` ticks (all arenas)
+        self.kl_ticks = horizon if old_logp == "fp32" else min(horizon, kl_ticks or max(1, horizon // 16))
         self.epochs, self.minibatches, self.clip = epochs, minibatches, clip
         self.vf_coef, self.ent_coef = vf_coef, ent_coef
         self.opt = torch.optim.Adam(list(self.actor.parameters()) + list(self.critic.parameters()), lr=lr)
@@ -221,7 +264,8 @@ class PPOTrainer:
         self._next_first = None
 
     def collect(self):
-        """One fused rollout; returns (features [T+1][N][8], actions, rewards, dones)."""
+        """One fused rollout; returns (features [T+1][N][8] f32, actions u8, rewards f64, dones u8)
+        as [T][N] device tensors (the trajectory's own buffers)."""
         torch = _torch()
         first = self._next_first if self._next_first is not None else obs_features(self.sim.outputs())
         self.rollout.rollout(self.horizon, self.actions, self.logp, trajectory=self.traj)
@@ -229,36 +273,42 @@ class PPOTrainer:
         T, N = self.horizon, self.sim.num_envs
         feats = torch.empty((T + 1, N, N_FEATURES), dtype=torch.float32, device=first.device)
         feats[0] = first
-        feats[1:] = torch.cat([tr["guard"].float() / 3.0, tr["move"].float() / 16.0, tr["move_frame"] / 55.0,
-                               tr["position"] / 4.6], dim=2)
+        f = feats[1:]  # obs_features of every tick, each pair written into its columns
+        torch.div(tr["guard"], 3.0, out=f[..., 0:2])
+        torch.div(tr["move"], 16.0, out=f[..., 2:4])
+        torch.div(tr["move_frame"], 55.0, out=f[..., 4:6])
+        torch.div(tr["position"], 4.6, out=f[..., 6:8])
         self._next_first = feats[T]
-        return feats, self.actions.long(), tr["reward"].float(), tr["terminated"].float()
+        return feats, self.actions, tr["reward"], tr["terminated"]
 
     def update(self, feats, actions, rewards, dones):
         torch = _torch()
         T, N = actions.shape
+        M = T * N
+        nk = self.kl_ticks * N  # samples with an fp32 log-prob (all of them in "fp32" mode)
         with torch.no_grad():
-            x = feats[:T].reshape(T * N, N_FEATURES)
-            a = actions.reshape(T * N)
-            if self._grad is not None:  # both forward passes in two fused launches
-                v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), self.actions.view(-1), T * N)
+            x = feats[:T].reshape(M, N_FEATURES)
+            a = actions.reshape(M)
+            behav = self.logp.reshape(M)  # what the kernel sampled with (bf16 actor)
+            if self._grad is not None:  # both forward passes, GAE and the sample table: five launches
+                v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk)
                 values = v.view(T + 1, N)
+                adv, ret = gae_device(rewards, dones, values, self.gamma, self.lam)
+                old = behav if self.old_logp == "behaviour" else old32
+                rows = pack_rows(x, a, old, adv.view(M), ret.view(M))
             else:
                 values = self.critic(feats).squeeze(-1)  # [T+1][N]
-                old32 = torch.log_softmax(self.actor(x), dim=1).gather(1, a[:, None])[:, 0]
-            adv, ret = gae(rewards, values, dones, self.gamma, self.lam)
-            behav = self.logp.reshape(T * N)  # what the kernel sampled with (bf16 actor)
-            gap = behav - old32
-            old = behav if self.old_logp == "behaviour" else old32
-            adv = adv.reshape(T * N)
-            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-            ret = ret.reshape(T * N)
-        M = T * N
+                old32 = torch.log_softmax(self.actor(x[:nk]), dim=1).gather(1, a[:nk, None].long())[:, 0]
+                adv, ret = gae(rewards.float(), values, dones.float(), self.gamma, self.lam)
+                old = behav if self.old_logp == "behaviour" else old32
+                adv = adv.reshape(M)
+                adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+                rows = torch.cat([x, a[:, None].float(), old[:, None], adv[:, None], ret.reshape(M, 1)], dim=1)  # [M, 12]
+            gap = behav[:nk] - old32
         # Minibatches: a random permutation of runs of _SHUFFLE_CHUNK consecutive samples (one tick,
         # that many consecutive arenas) when they tile the batch, so each minibatch is gathered as
         # whole runs (row copies) instead of 2 M scattered rows; per-sample otherwise.
         C = _SHUFFLE_CHUNK if M % (_SHUFFLE_CHUNK * self.minibatches) == 0 else 1
-        rows = torch.cat([x, a[:, None].float(), old[:, None], adv[:, None], ret[:, None]], dim=1)  # [M, 12]
         runs = rows.view(M // C, C, rows.shape[1])
         nb = (M // C + self.minibatches - 1) // self.minibatches
         for _ in range(self.epochs):
@@ -307,4 +357,4 @@ class PPOTrainer:
         return iterations * self.horizon * self.sim.num_envs / (time.perf_counter() - t0)
 
 
-__all__ = ["PPOTrainer", "PPOGrad", "make_critic", "gae", "N_ACTIONS"]
+__all__ = ["PPOTrainer", "PPOGrad", "make_critic", "gae", "gae_device", "pack_rows", "N_ACTIONS"]

@@ -306,6 +306,19 @@ int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_
 int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
                 float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
                 size_t workspace_bytes, void* stream);
+/* GAE of a [T][N] trajectory (ppo.py gae), asynchronously on `stream`: rewards device
+ * [T][N] f64 and done device [T][N] u8 as fs_step_n_policy's trajectory holds them, values
+ * device [T + 1][N] f32 (the last row bootstraps); delta = (r + (gamma v[t+1]) keep) - v[t],
+ * keep = 1 - done, adv[t] = delta[t] + gamma_lam keep[t] adv[t + 1] (one fused multiply-add),
+ * ret = adv + v[t].  gamma and gamma_lam (= gamma * lam) as the f32 values torch rounds them to. */
+int fs_ppo_gae(const double* rewards, const uint8_t* done, const float* values, int T, int64_t N, float gamma,
+               float gamma_lam, float* adv_out, float* ret_out, void* stream);
+/* fs_ppo_grad's [n][12] row table from its columns, asynchronously on `stream`: x device
+ * [n][8] f32 (16-byte aligned), actions u8 [n], old log-probs, advantages and returns f32 [n],
+ * stats device [2] f32 = (mean, std) of the advantages; row = x, action,
+ * old, (adv - mean) / (std + 1e-8), ret. */
+int fs_ppo_pack(const float* x, const uint8_t* actions, const float* old_logp, const float* adv, const float* ret,
+                const float* stats, int64_t n, float* rows_out, void* stream);
 
 /* Fill device arrays p1_out/p2_out [n_steps][N] with the synthetic action stream
  * of fs_step_n (splitmix64 hash of (seed, arena_base + i, t0 + k, player)),

@@ -152,3 +152,40 @@ def test_ppo_eval_matches_torch_forward(n, n_logp):
     torch.testing.assert_close(lp, lp_ref, rtol=RTOL, atol=1e-5)
     v2, lp2 = PPOGrad(actor, critic).evaluate(x)
     assert lp2 is None and torch.equal(v2, v)
+
+
+@pytest.mark.parametrize("T,N", [(1, 5), (17, 333), (128, 4096)])
+def test_ppo_gae_and_pack_match_torch(T, N):
+    """fs_ppo_gae against ppo.gae (the TD errors op for op; the recursion's fused multiply-add
+    against addcmul: rtol 1e-5, atol 1e-5 x the largest advantage), and fs_ppo_pack against the
+    torch.cat sample table with torch's normalisation: bit-exact on the same advantages."""
+    import torch
+    from footsies_gym_amd.ppo import gae, gae_device, pack_rows
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cuda").manual_seed(T * 1000 + N)
+    rew = torch.randn((T, N), generator=g, device=dev, dtype=torch.float64) * 0.3
+    rew[torch.rand((T, N), generator=g, device=dev) < 0.7] = 0.0
+    done = (torch.rand((T, N), generator=g, device=dev) < 0.05).to(torch.uint8)
+    val = torch.randn((T + 1, N), generator=g, device=dev)
+    adv, ret = gae_device(rew, done, val, 0.99, 0.95)
+    want_adv, want_ret = gae(rew.float(), val, done.float(), 0.99, 0.95)
+    tol = 1e-5 * float(want_adv.abs().max())
+    assert torch.allclose(adv, want_adv, rtol=1e-5, atol=tol)
+    assert torch.allclose(ret, want_ret, rtol=1e-5, atol=tol)
+    if T == 1:  # no recursion: every step is one rounding per op, as in gae()
+        assert torch.equal(adv, want_adv) and torch.equal(ret, want_ret)
+    M = T * N
+    x = torch.rand((M, 8), generator=g, device=dev)
+    a = torch.randint(0, 8, (M,), generator=g, device=dev, dtype=torch.uint8)
+    old = torch.randn(M, generator=g, device=dev)
+    if M < 2:
+        return  # (torch's std of one sample is nan; the trainer's batches are large)
+    rows = pack_rows(x, a, old, adv.view(M), ret.view(M))
+    an = adv.view(M)
+    an = (an - an.mean()) / (an.std() + 1e-8)
+    want = torch.cat([x, a[:, None].float(), old[:, None], an[:, None], ret.view(M, 1)], dim=1)
+    assert torch.equal(rows, want)
+    with pytest.raises(ValueError):
+        pack_rows(x, a.long(), old, adv.view(M), ret.view(M))
+    with pytest.raises(ValueError):
+        gae_device(rew.float(), done, val, 0.99, 0.95)
