@@ -541,6 +541,20 @@ FS_API int fs_ppo_gae(const double* rewards, const uint8_t* done, const float* v
   return FS_OK;
 }
 
+FS_API int fs_ppo_features(const uint8_t* guard, const uint8_t* move, const float* move_frame, const float* position,
+                           int64_t n, float* out, void* stream) {
+  if (!guard || !move || !move_frame || !position || !out || n <= 0)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_features: all five arrays and n > 0 required");
+  if (reinterpret_cast<uintptr_t>(out) % 16 || reinterpret_cast<uintptr_t>(move_frame) % 8 ||
+      reinterpret_cast<uintptr_t>(position) % 8 || reinterpret_cast<uintptr_t>(guard) % 2 ||
+      reinterpret_cast<uintptr_t>(move) % 2)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_features: misaligned array");
+  const hipError_t e = fsk::launch_ppo_features(guard, move, move_frame, position, n, out,
+                                                static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_features: %s", hipGetErrorString(e));
+  return FS_OK;
+}
+
 FS_API int fs_ppo_pack(const float* x, const uint8_t* actions, const float* old_logp, const float* adv,
                        const float* ret, const float* stats, int64_t n, float* rows_out, void* stream) {
   if (!x || !actions || !old_logp || !adv || !ret || !stats || !rows_out || n <= 0)

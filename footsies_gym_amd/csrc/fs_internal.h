@@ -138,6 +138,8 @@ hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* acti
                            hipStream_t s);
 hipError_t launch_ppo_gae(const double* rew, const uint8_t* done, const float* val, int T, int64_t N, float gamma,
                           float gamma_lam, float* adv, float* ret, hipStream_t s);
+hipError_t launch_ppo_features(const uint8_t* guard, const uint8_t* move, const float* move_frame,
+                               const float* position, int64_t n, float* out, hipStream_t s);
 hipError_t launch_ppo_pack(const float* x, const uint8_t* act, const float* old, const float* adv, const float* ret,
                            const float* stats, int64_t n, float* rows, hipStream_t s);
 

@@ -497,9 +497,35 @@ __global__ __launch_bounds__(256) void k_ppo_pack(const float* __restrict__ x, c
   out[2] = make_float4((float)act[m], old[m], (adv[m] - mean) / den, ret[m]);
 }
 
+// obs_features (rollout.py) of n observations: guard / 3, move / 16, move_frame / 55, position / 4.6
+// for both fighters, each as torch's division by a host scalar computes it on the GPU: x times the
+// f64 reciprocal of the divisor rounded to f32 (neither x / b nor x * (1.0f / b) agrees for 4.6).
+__global__ __launch_bounds__(256) void k_ppo_features(const uint8_t* __restrict__ guard, const uint8_t* __restrict__ move,
+                                                      const float* __restrict__ move_frame,
+                                                      const float* __restrict__ position, int64_t n,
+                                                      float* __restrict__ out) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  const uchar2 g = reinterpret_cast<const uchar2*>(guard)[m];
+  const uchar2 mv = reinterpret_cast<const uchar2*>(move)[m];
+  const float2 f = reinterpret_cast<const float2*>(move_frame)[m];
+  const float2 p = reinterpret_cast<const float2*>(position)[m];
+  float4* o = reinterpret_cast<float4*>(out + m * kF);
+  constexpr float r3 = (float)(1.0 / 3.0), r16 = (float)(1.0 / 16.0), r55 = (float)(1.0 / 55.0), r46 = (float)(1.0 / 4.6);
+  o[0] = make_float4((float)g.x * r3, (float)g.y * r3, (float)mv.x * r16, (float)mv.y * r16);
+  o[1] = make_float4(f.x * r55, f.y * r55, p.x * r46, p.y * r46);
+}
+
 }  // namespace fsl
 
 namespace fsk {
+
+hipError_t launch_ppo_features(const uint8_t* guard, const uint8_t* move, const float* move_frame,
+                               const float* position, int64_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(fsl::k_ppo_features, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, guard, move, move_frame,
+                     position, n, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_ppo_gae(const double* rew, const uint8_t* done, const float* val, int T, int64_t N, float gamma,
                           float gamma_lam, float* adv, float* ret, hipStream_t s) {

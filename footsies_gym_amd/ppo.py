@@ -206,6 +206,24 @@ def gae_device(rewards, dones, values, gamma, lam):
     return adv, ret
 
 
+def features_device(tr, out):
+    """obs_features of every [T][N] trajectory row in one launch (fs_ppo_features) into out
+    [T][N][8] f32, bit-identical to the torch ops (each division by a host scalar is torch's
+    x * f32(1 / b), the reciprocal taken in f64)."""
+    torch = _torch()
+    cols = (tr["guard"], tr["move"], tr["move_frame"], tr["position"])
+    n = out.numel() // N_FEATURES
+    if (out.dtype != torch.float32 or not out.is_contiguous() or out.shape[-1] != N_FEATURES
+            or not all(t.is_contiguous() and t.numel() == 2 * n for t in cols)
+            or cols[0].dtype != torch.uint8 or cols[1].dtype != torch.uint8
+            or cols[2].dtype != torch.float32 or cols[3].dtype != torch.float32):
+        raise ValueError("features_device: contiguous u8 guard / move, f32 move_frame / position [..][2], f32 out [..][8]")
+    stream = torch.cuda.current_stream(out.device).cuda_stream
+    check(lib().fs_ppo_features(*[C.c_void_p(t.data_ptr()) for t in cols], n, C.c_void_p(out.data_ptr()),
+                                C.c_void_p(stream)))
+    return out
+
+
 def pack_rows(x, actions, old, adv, ret, out=None):
     """fs_ppo_grad's [M, 12] sample table in one launch (fs_ppo_pack): x [M, 8] f32, actions u8
     [M], old log-probs, advantages and returns f32 [M]; the advantages normalised on the way as
@@ -273,11 +291,14 @@ class PPOTrainer:
         T, N = self.horizon, self.sim.num_envs
         feats = torch.empty((T + 1, N, N_FEATURES), dtype=torch.float32, device=first.device)
         feats[0] = first
-        f = feats[1:]  # obs_features of every tick, each pair written into its columns
-        torch.div(tr["guard"], 3.0, out=f[..., 0:2])
-        torch.div(tr["move"], 16.0, out=f[..., 2:4])
-        torch.div(tr["move_frame"], 55.0, out=f[..., 4:6])
-        torch.div(tr["position"], 4.6, out=f[..., 6:8])
+        if self._grad is not None:
+            features_device(tr, feats[1:])  # obs_features of every tick, one launch
+        else:
+            f = feats[1:]  # each pair written into its columns
+            torch.div(tr["guard"], 3.0, out=f[..., 0:2])
+            torch.div(tr["move"], 16.0, out=f[..., 2:4])
+            torch.div(tr["move_frame"], 55.0, out=f[..., 4:6])
+            torch.div(tr["position"], 4.6, out=f[..., 6:8])
         self._next_first = feats[T]
         return feats, self.actions, tr["reward"], tr["terminated"]
 
@@ -357,4 +378,4 @@ class PPOTrainer:
         return iterations * self.horizon * self.sim.num_envs / (time.perf_counter() - t0)
 
 
-__all__ = ["PPOTrainer", "PPOGrad", "make_critic", "gae", "gae_device", "pack_rows", "N_ACTIONS"]
+__all__ = ["PPOTrainer", "PPOGrad", "make_critic", "gae", "gae_device", "pack_rows", "features_device", "N_ACTIONS"]

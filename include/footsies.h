@@ -313,6 +313,12 @@ int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp*
  * ret = adv + v[t].  gamma and gamma_lam (= gamma * lam) as the f32 values torch rounds them to. */
 int fs_ppo_gae(const double* rewards, const uint8_t* done, const float* values, int T, int64_t N, float gamma,
                float gamma_lam, float* adv_out, float* ret_out, void* stream);
+/* The learner's features of n observations, asynchronously on `stream`: out device [n][8] f32
+ * (16-byte aligned) = guard / 3, move / 16, move_frame / 55, position / 4.6 of both fighters
+ * (wrappers/normalization.py's constants), each x * f32(1 / divisor in f64) as torch computes it; inputs are
+ * trajectory columns ([n][2] u8, u8, f32, f32). */
+int fs_ppo_features(const uint8_t* guard, const uint8_t* move, const float* move_frame, const float* position,
+                    int64_t n, float* out, void* stream);
 /* fs_ppo_grad's [n][12] row table from its columns, asynchronously on `stream`: x device
  * [n][8] f32 (16-byte aligned), actions u8 [n], old log-probs, advantages and returns f32 [n],
  * stats device [2] f32 = (mean, std) of the advantages; row = x, action,

@@ -189,3 +189,22 @@ def test_ppo_gae_and_pack_match_torch(T, N):
         pack_rows(x, a.long(), old, adv.view(M), ret.view(M))
     with pytest.raises(ValueError):
         gae_device(rew.float(), done, val, 0.99, 0.95)
+
+
+def test_ppo_features_match_obs_features():
+    """fs_ppo_features against rollout.obs_features (torch's divisions by host scalars) on every
+    trajectory row of a short policy rollout: bit-exact."""
+    import torch
+    from footsies_gym_amd.ppo import features_device
+    from footsies_gym_amd.rollout import FusedPolicyRollout, make_actor, obs_features
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(3001, p2_mode="bot", seed=11)
+    T = 40
+    tr = sim.alloc_trajectory(T)
+    FusedPolicyRollout(sim, make_actor(device=sim.device, seed=4), seed=2).rollout(T, trajectory=tr)
+    out = torch.empty((T, sim.num_envs, 8), dtype=torch.float32, device=sim.device)
+    features_device(tr, out)
+    for t in (0, 7, T - 1):
+        assert torch.equal(out[t], obs_features({k: tr[k][t] for k in ("guard", "move", "move_frame", "position")}))
+    with pytest.raises(ValueError):
+        features_device(tr, out[:, :, :4])
