@@ -446,8 +446,11 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
   const int p = blockIdx.x * 64 + pl;
   constexpr int P = n_params<OUT>(), S = partial_stride<OUT>();
   float a = 0.f;
-  if (p < P + 3)
+  if (p < P + 3) {
+    // unrolled so eight loads are in flight per thread; the additions keep their order
+#pragma unroll 8
     for (int w = g; w < waves; w += 16) a += partial[(size_t)w * S + p];
+  }
   sum[g][pl] = a;
   __syncthreads();
   if (g == 0 && p < P + 3) {
