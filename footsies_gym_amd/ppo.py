@@ -268,7 +268,9 @@ class PPOTrainer:
         self.kl_ticks = horizon if old_logp == "fp32" else min(horizon, kl_ticks or max(1, horizon // 16))
         self.epochs, self.minibatches, self.clip = epochs, minibatches, clip
         self.vf_coef, self.ent_coef = vf_coef, ent_coef
-        self.opt = torch.optim.Adam(list(self.actor.parameters()) + list(self.critic.parameters()), lr=lr)
+        # one fused kernel per step on the device instead of ~7 foreach launches
+        self.opt = torch.optim.Adam(list(self.actor.parameters()) + list(self.critic.parameters()), lr=lr,
+                                    fused=dev.type == "cuda")
         self._grad = PPOGrad(self.actor, self.critic) if learner == "hip" else None
         self.traj = sim.alloc_trajectory(horizon)
         n = sim.num_envs
