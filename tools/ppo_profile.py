@@ -24,7 +24,8 @@ def main():
     import torch
     from torch.profiler import ProfilerActivity, profile
 
-    from footsies_gym_amd.ppo import PPOTrainer, gae
+    from footsies_gym_amd.ppo import PPOTrainer, gae_device
+    from footsies_gym_amd.rollout import N_FEATURES
     from footsies_gym_amd.simulator import FootsiesSim
 
     sim = FootsiesSim(args.envs, device=0, p2_mode="bot", seed=0)
@@ -39,10 +40,10 @@ def main():
         a = now()
         feats, actions, rewards, dones = tr.collect()
         b = now()
-        with torch.no_grad():
-            values = tr.critic(feats).squeeze(-1)
+        with torch.no_grad():  # the trainer's own launches (learner="hip")
+            values, _ = tr._grad.evaluate(feats.view(-1, N_FEATURES))
             c = now()
-            gae(rewards, values, dones, tr.gamma, tr.lam)
+            gae_device(rewards, dones, values.view(-1, sim.num_envs), tr.gamma, tr.lam)
             d = now()
         tr.update(feats, actions, rewards, dones)
         e = now()
