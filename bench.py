@@ -14,8 +14,11 @@ Modes
   step:            fs_step, one kernel launch per tick (the VectorEnv.step path).
 Both modes are timed and reported; `value` is the --mode one.
 
-Multi-GPU: one process per GPU (torch.distributed.run), arenas sharded per rank
-with no data-path collective (`scaling: weak`); max-over-ranks timing.
+Multi-GPU: one process per GPU, arenas sharded per rank with no data-path collective
+(`scaling: weak`); max-over-ranks timing.  `python bench.py --gpus N` starts the N ranks
+itself (a torch.distributed.run child, started before this process touches the GPU);
+under an outside launcher (WORLD_SIZE set) it is one of the ranks and checks that the
+launcher's world size is N.
 """
 import argparse
 import ctypes as C
@@ -57,7 +60,31 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the C2 bot-opponent and C5 policy-loop rates")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rehearse the launch / barrier / max-over-ranks / JSON plumbing with a no-op CPU step "
+                         "(no GPU, no simulator; the line says dry_run and is never a measurement)")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without an outside launcher: start N ranks, one per GPU, as one
+    torch.distributed.run child process and return its exit code.  Called before anything
+    touches the GPU (this process never initialises HIP), and the ranks are children, not
+    an exec of this process."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
 
 
 def cpu_baseline(envs, seconds, seed):
@@ -307,13 +334,65 @@ def issue_profile(kernel, envs, ticks):
     return best
 
 
+def dry_run(args, world, rank):
+    """The multi-rank plumbing without a GPU: the same regions (barrier on both sides, host wall
+    clock, max over ranks), a no-op CPU step, one JSON line from rank 0 marked dry_run."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    K, R, N = args.steps, max(1, args.regions), args.envs
+    x = torch.zeros(64)
+    walls, local = [], []
+    for _ in range(R):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            x.add_(1.0)
+        if world > 1:
+            dist.barrier()
+        local.append(time.perf_counter() - t0)
+        t = torch.tensor([local[-1]], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        walls.append(float(t.item()))
+    wall = sorted(walls)[len(walls) // 2]
+    mine = torch.tensor([float(N), sorted(local)[len(local) // 2]], dtype=torch.float64)
+    every = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(every, mine)
+    else:
+        every = [mine]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": sum(float(e[0]) for e in every) * K / wall, "unit": "env-steps/s",
+                          "n_gpus": world, "steps": K, "warmup": args.warmup, "ms_per_step": 1e3 * wall / K,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dry_run": True,
+                          "dtype": "none (dry run)", "data": "none (dry run: no-op CPU step, not a measurement)",
+                          "config": {"workload": "dry run", "envs_per_gpu": N, "global_envs": N * world,
+                                     "parallelism": "arena-shard x%d" % world},
+                          "ranks": {"world_size": world, "backend": dist.get_backend() if world > 1 else None,
+                                    "rank_walls_ms": [round(1e3 * float(e[1]), 4) for e in every]}}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's plain `python3 bench.py --gpus N`: start the N ranks (nothing has touched the GPU)
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py --gpus %d, but the launcher started %d rank(s) (WORLD_SIZE)" % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; the modulo only matters when ranks are rehearsed on fewer devices
     local = local % max(1, torch.cuda.device_count())
@@ -387,10 +466,20 @@ def main():
         torch.cuda.synchronize(dev)
         barrier()
         wall = time.perf_counter() - t0
+        local_walls.append(wall)
         t = torch.tensor([wall], dtype=torch.float64, device=coll_dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    def rank_values(v):
+        """Every rank's value of v (this rank's median region wall), in rank order, in ms."""
+        t = torch.tensor([v], dtype=torch.float64, device=coll_dev)
+        if world == 1:
+            return [round(1e3 * v, 4)]
+        every = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(every, t)
+        return [round(1e3 * float(e.item()), 4) for e in every]
 
     def kernel_time(fn, lo, hi, launches, ticks_per_launch):
         """Average kernel duration with the queue pre-filled (a spin kernel holds the GPU while
@@ -419,10 +508,13 @@ def main():
     # median region is reported, every region's wall time is listed
     res = {}
     for mode, fn in (("fused", run_fused), ("step", run_step)):
+        local_walls = []
         walls = [timed(fn, W + r * K, K) for r in range(R)]
         wall = sorted(walls)[len(walls) // 2]
+        mine = sorted(local_walls)[len(local_walls) // 2]
         res[mode] = {"wall_s": wall, "region_walls_ms": [round(1e3 * w, 4) for w in walls],
-                     "env_steps_per_s": world * N * K / wall, "ms_per_step": 1e3 * wall / K}
+                     "env_steps_per_s": world * N * K / wall, "ms_per_step": 1e3 * wall / K,
+                     "rank_walls_ms": rank_values(mine)}
     # P1/P2 actions handed over from host memory (FS_ACT_HOST: pinned staging + H2D copy per
     # step), the PCIe-inclusive rate of the per-step path; reported beside, never as `value`
     kh = min(K, 500)
@@ -510,6 +602,11 @@ def main():
                                 "C3: %d arenas/GPU" % N) + ", self-play random actions, P2 external, auto-reset same-step",
                    "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
                    "ticks_per_launch": chunk if args.mode == "fused" else 1, "parallelism": "arena-shard x%d" % world},
+        "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,
+                  "backend": dist.get_backend() if world > 1 else None,
+                  "rank_walls_ms": res[args.mode]["rank_walls_ms"],
+                  "note": "world_size / backend as the process group reports them (nccl = RCCL); each rank's "
+                          "median region wall, before the max over ranks"},
         "timing": {"regions": R, "region_walls_ms": res[args.mode]["region_walls_ms"],
                    "note": "each region times exactly `steps` steps between barrier + synchronize pairs "
                            "(host wall clock, max over ranks); value = the median region"},

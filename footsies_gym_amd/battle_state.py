@@ -32,6 +32,9 @@ from typing import List
 
 import numpy as np
 
+from . import _abi
+from ._lib import FootsiesError
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INPUT_RECORD_FRAME = 180  # Fighter.inputRecordFrame (Fighter.cs:98-101)
 MAX_SPRITE_SHAKE_FRAME = 6  # Fighter.cs:110
@@ -137,9 +140,35 @@ def dumps(state):
     return enc(state)
 
 
-def _load_fighter(dst, s):
-    """Fighter.LoadState (Fighter.cs:741-811) onto one fs_fighter_state record."""
-    dst["position_x"] = np.float32(s["position"][0])
+class UnsupportedBattleStateError(FootsiesError, ValueError):
+    """A BattleState the simulator cannot continue exactly: Fighter.LoadState (Fighter.cs:741-744)
+    restores position.y and isFaceRight, but every state the game itself produces has y == 0 and
+    P1 facing right / P2 left (SetupBattleStart, Fighter.cs:120-135; nothing moves y or turns a
+    fighter).  A non-zero y would matter from the next tick on -- ApplyPositionChange(dx,
+    position.y) adds it on every push, and fighter2's mirrored push uses fighter1's y
+    (BattleCore.cs:492-498) -- and a flipped facing mirrors every box and input, so such a
+    state is refused rather than silently continued as a different game."""
+
+    def __init__(self, message):
+        FootsiesError.__init__(self, _abi.FS_E_UNSUPPORTED, message)
+
+
+def _load_fighter(dst, s, is_p1):
+    """Fighter.LoadState (Fighter.cs:741-811) onto one fs_fighter_state record.  Raises
+    UnsupportedBattleStateError for a position.y other than 0 or a non-standard facing."""
+    who = "p1State" if is_p1 else "p2State"
+    pos = list(s["position"])
+    if len(pos) != 2:
+        raise UnsupportedBattleStateError("%s.position must be [x, y], got %r" % (who, pos))
+    if np.float32(pos[1]) != 0:
+        raise UnsupportedBattleStateError(
+            "%s.position[1] = %r: the simulator keeps fighters on the ground (y = 0, as every state the game "
+            "produces); a non-zero y would shift every later push (BattleCore.cs:492-498)" % (who, pos[1]))
+    if bool(s["isFaceRight"]) != is_p1:
+        raise UnsupportedBattleStateError(
+            "%s.isFaceRight = %r: P1 always faces right and P2 left (Fighter.cs:124); a flipped fighter is "
+            "not supported" % (who, s["isFaceRight"]))
+    dst["position_x"] = np.float32(pos[0])
     dst["action_id"] = int(s["currentActionID"])
     dst["action_frame"] = int(s["currentActionFrame"])
     dst["hit_count"] = int(s["currentActionHitCount"])
@@ -168,8 +197,8 @@ def load_into(states, i, state):
     BattleState dict or its JSON text."""
     if isinstance(state, str):
         state = json.loads(state)
-    _load_fighter(states[i]["f"][0], state["p1State"])
-    _load_fighter(states[i]["f"][1], state["p2State"])
+    _load_fighter(states[i]["f"][0], state["p1State"], True)
+    _load_fighter(states[i]["f"][1], state["p2State"], False)
     states["frame_count"][i] = int(state["frameCount"])
     return states
 

@@ -1241,7 +1241,9 @@ __device__ __forceinline__ uint32_t hash_action(uint64_t seed, uint64_t env, uin
 // terminated, truncated) and tick t+2's load -- so the row is resident while those stores may
 // still be in flight.  The loaded register is read by nothing but the wait statement, which copies
 // the row out after the s_waitcnt; tools/check_async_loads.py checks on the assembly that no
-// instruction touches a register between its load and its wait (tests/test_async_loads.py).
+// instruction touches a register between its load and its wait, and that on every path at least
+// 11 vector memory instructions are issued between each row load and its wait
+// (tests/test_async_loads.py).
 __device__ __forceinline__ uint32_t row_load(const uint8_t* p) {
   uint32_t v;
   asm volatile("global_load_ubyte %0, %1, off" : "=v"(v) : "v"(p) : "memory");
@@ -1258,6 +1260,25 @@ __device__ __forceinline__ void settle_w(uint32_t& next) {
     asm volatile("s_waitcnt vmcnt(%2)\n\tv_mov_b32 %0, %1" : "=v"(ready) : "v"(next), "n"(WAIT) : "memory");
     next = ready;
   }
+}
+
+// Time-sliced wave priority.  At C3's 65 536 arenas each SIMD holds two waves of the fused loop,
+// one from block b and one from block b + 256 (256 CUs).  With equal priorities the sequencer
+// favours the older wave, so it runs ~11 % ahead and finishes first, and the younger one runs its
+// last ~10 % of ticks alone on the SIMD, where one wave cannot issue as fast as two
+// (tools/timeline_probe.py: loop times 988 vs 1099 us of a 1000-tick launch, 17.9 vs 22.1 us of a
+// 20-tick one).  Every tick each wave raises its priority in alternate 2^9 / 100 MHz = 5.1 us
+// slices of the constant clock all CUs share, the two waves of a SIMD (wave slots of opposite
+// parity) in opposite slices, so both progress at the same rate and finish together.
+// (+4.8 % at 1000 ticks per launch, +3.4 % at 20; slices of 0.64 us: +0.4 %.)
+constexpr int kPrioSliceShift = 9;
+__device__ __forceinline__ uint32_t prio_group() {
+  return __builtin_amdgcn_s_getreg(4 /* HW_ID */ | (31 << 11)) & 1u;  // bit 0 of the wave slot
+}
+__device__ __forceinline__ void prio_slice(uint32_t grp) {
+  const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  if (((now >> kPrioSliceShift) ^ grp) & 1u) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
 }
 
 // The burst leaves mostly constants in the lane (SetupBattleStart, STAND's ActionInfo).  Where
@@ -1476,9 +1497,11 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     uint32_t d0, d1;
     policy_features(L, d0, d1);
     const PolicyWeights W = policy_weights();
+    const uint32_t grp = prio_group();
     for (int t = 0; t < p.n_steps; t++) {
       const uint32_t act = next;
       next = fetch(min(t + 1, p.n_steps - 1));
+      prio_slice(grp);
       const PolicyOut po = policy_act(W, d0, d1, p.pol.seed, p.arena_base + arena0, p.t0 + (uint64_t)t);
       if (active) {
         const uint32_t row = (uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a;
@@ -1493,9 +1516,11 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   } else if constexpr (FUSED) {
     const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
     if constexpr (HASH) {
+      const uint32_t grp = prio_group();
       for (int t = 0; t < p.n_steps; t++) {
         const uint32_t act = next;
         next = fetch(min(t + 1, p.n_steps - 1));
+        prio_slice(grp);
         env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
       }
     } else {
@@ -1508,12 +1533,15 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       uint32_t a_fl = next, b_fl = row1, a_rd, b_rd;
       asm volatile("s_waitcnt vmcnt(0)\n\tv_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(a_rd), "=v"(b_rd)
                    : "v"(a_fl), "v"(b_fl) : "memory");
+      const uint32_t grp = prio_group();
       int t = 0;
       for (; t < last; t += 2) {
         a_fl = issue(t + 2);
+        prio_slice(grp);
         env_step<FM, P2, 11>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
         b_rd = b_fl;
         b_fl = issue(t + 3);
+        prio_slice(grp);
         env_step<FM, P2, 11>(L, reads ? b_rd & 7u : 0u, p, (uint32_t)(t + 1) * row_step + (uint32_t)a, a_fl);
         a_rd = a_fl;
       }

@@ -27,6 +27,25 @@ _ATTACK_FRAMES = {"N_ATTACK": (4, 2, 16), "B_ATTACK": (3, 3, 15), "N_SPECIAL": (
 
 FootsiesMove = Enum("FootsiesMove", [(name, FootsiesMoveInfo(mid, dur, *_ATTACK_FRAMES.get(name, (0, 0, 0))))
                                      for name, mid, dur in MOVES])
+
+
+# the reference's phase tests (moves.py:31-38), by frame of the move
+def _in_recovery(self, frame: int) -> bool:
+    return frame >= (self.value.startup + self.value.active)
+
+
+def _in_active(self, frame: int) -> bool:
+    return self.value.startup <= frame < (self.value.startup + self.value.active)
+
+
+def _in_startup(self, frame: int) -> bool:
+    return frame < self.value.startup
+
+
+FootsiesMove.in_recovery = _in_recovery
+FootsiesMove.in_active = _in_active
+FootsiesMove.in_startup = _in_startup
+
 FOOTSIES_MOVE_INDEX_TO_MOVE = list(FootsiesMove)
 FOOTSIES_MOVE_ID_TO_INDEX = {m.value.id: i for i, m in enumerate(FOOTSIES_MOVE_INDEX_TO_MOVE)}
 

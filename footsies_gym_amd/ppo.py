@@ -136,8 +136,30 @@ class PPOGrad:
         assert off == self.grad.numel()
         self.loss = torch.zeros(3, dtype=torch.float32, device=dev)
         self.workspace = torch.empty(lib().fs_ppo_workspace_bytes(), dtype=torch.uint8, device=dev)
-        self._mlps = [_abi.fs_mlp(*[t.data_ptr() for t in params]) for params in nets]
+        self._nets = nets
+        self._bind()
         self.device = dev
+
+    def _bind(self):
+        """The kernels' view of the parameters: raw device pointers of every weight and bias."""
+        self._mlps = [_abi.fs_mlp(*[t.data_ptr() for t in params]) for params in self._nets]
+        self._ptrs = [p.data_ptr() for p in self.params]
+
+    def _check_bindings(self):
+        """Before a launch: every parameter's .grad must still be its view of the flat buffer the
+        kernel writes (an optimizer's zero_grad(set_to_none=True) drops it; it is re-attached --
+        the kernel overwrites the whole buffer), and every parameter must still live where the
+        kernel reads it (param.data = ..., .to(): the pointers are re-read)."""
+        off = 0
+        base = self.grad.data_ptr()
+        for p in self.params:
+            if p.grad is None or p.grad.data_ptr() != base + 4 * off or p.grad.shape != p.shape:
+                p.grad = self.grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        if [p.data_ptr() for p in self.params] != self._ptrs:
+            if any(t.dtype != _torch().float32 or not t.is_cuda or not t.is_contiguous() for t in self.params):
+                raise ValueError("the fused learner needs contiguous fp32 device parameters")
+            self._bind()
 
     def evaluate(self, x, actions=None, n_logp=0):
         """fs_ppo_eval: (critic(x) [n], log_softmax(actor(x[:n_logp]))[actions] [n_logp] or None),
@@ -152,6 +174,7 @@ class PPOGrad:
             if actions is None or actions.dtype != torch.uint8 or actions.numel() < n_logp or not actions.is_contiguous():
                 raise ValueError("actions must be a contiguous uint8 tensor of at least n_logp entries")
             logp = torch.empty(n_logp, dtype=torch.float32, device=x.device)
+        self._check_bindings()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         check(lib().fs_ppo_eval(C.c_void_p(x.data_ptr()), n, C.c_void_p(actions.data_ptr() if n_logp else None),
                                 n_logp, C.byref(self._mlps[0]), C.byref(self._mlps[1]), C.c_void_p(values.data_ptr()),
@@ -163,6 +186,7 @@ class PPOGrad:
         torch = _torch()
         if rows.dtype != torch.float32 or rows.dim() != 2 or rows.shape[1] != 12 or not rows.is_contiguous():
             raise ValueError("rows must be a contiguous [n, 12] float32 tensor")
+        self._check_bindings()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         check(lib().fs_ppo_grad(C.c_void_p(rows.data_ptr()), rows.shape[0], C.byref(self._mlps[0]),
                                 C.byref(self._mlps[1]), clip, vf_coef, ent_coef, C.c_void_p(self.grad.data_ptr()),
@@ -255,6 +279,8 @@ class PPOTrainer:
             raise ValueError("old_logp must be 'behaviour' or 'fp32'")
         if learner not in ("hip", "torch"):
             raise ValueError("learner must be 'hip' or 'torch'")
+        if int(epochs) < 1 or int(minibatches) < 1 or int(horizon) < 1:
+            raise ValueError("PPOTrainer needs epochs >= 1, minibatches >= 1 and horizon >= 1")
         self.learner = learner
         self.old_logp = old_logp
         dev = sim.device
@@ -289,6 +315,9 @@ class PPOTrainer:
         torch = _torch()
         first = self._next_first if self._next_first is not None else obs_features(self.sim.outputs())
         self.rollout.rollout(self.horizon, self.actions, self.logp, trajectory=self.traj)
+        cur = torch.cuda.current_stream(self.sim.device)
+        if cur != self.sim.stream:  # the trajectory was written on the handle's stream
+            cur.wait_stream(self.sim.stream)
         tr = self.traj
         T, N = self.horizon, self.sim.num_envs
         feats = torch.empty((T + 1, N, N_FEATURES), dtype=torch.float32, device=first.device)

@@ -118,6 +118,12 @@ class FootsiesSim:
         torch = _torch()
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         check(lib().fs_set_stream(self._h, C.c_void_p(s.cuda_stream)), self._h)
+        self._stream = s
+
+    @property
+    def stream(self):
+        """The torch stream the library issues this handle's kernels on (use_torch_stream)."""
+        return self._stream
 
     # -- core API --------------------------------------------------------------------
     def reset(self, seeds=None, mask=None, hard=False, seed_only=False):
@@ -234,7 +240,10 @@ class FootsiesSim:
         if self._host_buf is None:
             self._host_buf = torch.empty(self._out_buf.numel(), dtype=torch.uint8, pin_memory=True)
             self._host_np = self._host_buf.numpy()
-        self._host_buf.copy_(self._out_buf)  # ordered after the library's work on this stream
+        # on the handle's own stream, so the copy is ordered after the library's kernels whatever
+        # torch's current stream is (a blocking copy: it returns once the bytes are on the host)
+        with torch.cuda.stream(self._stream):
+            self._host_buf.copy_(self._out_buf)
         out = {}
         for name, dt, shape, off, nbytes in self._out_layout:
             v = self._host_np[off:off + nbytes].view(dt).reshape(shape)

@@ -278,8 +278,29 @@ class FootsiesEnv(_EnvBase):
     render_mode = None  # rendering is the Unity window's (out of scope)
     spec = None
 
-    def __init__(self, frame_delay=0, dense_reward=True, opponent=None, device=0, seed=0, by_example=False,
-                 render_mode=None, **_unused):
+    VALID_SYNC_MODES = frozenset({"async", "synced_non_blocking", "synced_blocking"})
+
+    def __init__(self, frame_delay=0, render_mode=None, game_path="./Build/FOOTSIES", game_address="localhost",
+                 game_port=11000, skip_instancing=False, fast_forward=True, fast_forward_speed=6.0,
+                 sync_mode="synced_non_blocking", remote_control_port=11002, by_example=False, opponent=None,
+                 opponent_port=11001, vs_player=False, dense_reward=True, log_file=None, log_file_overwrite=False,
+                 device=0, seed=0):
+        """The reference's constructor (FE:34-53), in its order, plus ``device`` / ``seed``.  The
+        arguments that configure the game process and its sockets (game_path .. remote_control_port,
+        opponent_port, log_file*) are validated and recorded as FE does, and have no effect: the
+        game is the in-process simulator, always stepped in lockstep with the agent."""
+        # FE:100-108, same checks in the same order and the same exceptions
+        if sync_mode not in self.VALID_SYNC_MODES:
+            raise ValueError("sync mode '%s' is invalid, must be one of %s" % (sync_mode, set(self.VALID_SYNC_MODES)))
+        if opponent is not None and vs_player:
+            raise ValueError("custom opponent and human opponent can't be specified together")
+        if vs_player:  # a human P2 needs the game window (out of scope, DESIGN.md section 8)
+            raise ValueError("vs_player=True needs a human at the game window; the simulator has no human P2")
+        self.game_path, self.game_address, self.game_port = game_path, game_address, game_port
+        self.skip_instancing, self.fast_forward, self.fast_forward_speed = skip_instancing, fast_forward, fast_forward_speed
+        self.sync_mode, self.remote_control_port, self.opponent_port = sync_mode, remote_control_port, opponent_port
+        self.by_example, self.vs_player, self.dense_reward = by_example, vs_player, dense_reward
+        self.log_file, self.log_file_overwrite = log_file, log_file_overwrite
         # FE:133-134; "human" rendering is the Unity window's: accepted and recorded, nothing is drawn
         assert render_mode is None or render_mode in self.metadata["render_modes"]
         self.render_mode = render_mode

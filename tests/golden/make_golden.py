@@ -157,13 +157,9 @@ def main():
     data.update(generate("bot_delay1", _abi.FS_P2_BOT, False, 16, 1200, 4, 0.6, frame_delay=1))
     data.update(generate("ext_delay16", _abi.FS_P2_EXTERNAL, True, 8, 800, 5, 0.5, frame_delay=16))
     np.savez_compressed(os.path.join(HERE, "fe_golden.npz"), **data)
-    moves = {
-        "id_to_index": {str(k): v for k, v in ref_moves.FOOTSIES_MOVE_ID_TO_INDEX.items()},
-        "moves": [[m.name, m.value.id, m.value.duration, m.value.startup, m.value.active, m.value.recovery]
-                  for m in ref_moves.FootsiesMove],
-    }
-    with open(os.path.join(HERE, "moves_golden.json"), "w") as f:
-        json.dump(moves, f, indent=1)
+    sys.path.insert(0, HERE)
+    import make_moves_golden  # noqa: E402
+    make_moves_golden.write(ref_moves)
     print("wrote fe_golden.npz, moves_golden.json")
 
 

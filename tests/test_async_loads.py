@@ -14,3 +14,18 @@ def test_no_register_touched_while_its_row_is_in_flight():
                        text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " 0 findings" in r.stdout and "8 kernels" in r.stdout, r.stdout
+
+
+def test_wait_counts_are_proven_and_a_too_deep_wait_is_caught(tmp_path):
+    """The same analysis proves every `s_waitcnt vmcnt(11)` row wait: on every path at least 11
+    vector memory instructions follow the row's load (advisor r02).  A copy of the kernel whose
+    waits claim 30 (more than the stores of one tick plus a load) must be reported."""
+    src = os.path.join(ROOT, "footsies_gym_amd", "csrc", "fs_kernels.hip")
+    text = open(src).read()
+    assert text.count("env_step<FM, P2, 11>") >= 3
+    bad = tmp_path / "fs_kernels.hip"
+    bad.write_text(text.replace("env_step<FM, P2, 11>", "env_step<FM, P2, 30>"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_async_loads.py"), str(bad)],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 1, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "vmcnt(30) copies" in r.stdout, r.stdout[-2000:]

@@ -14,9 +14,15 @@ It builds each kernel's control-flow graph from the labels and branches, and pro
 of registers with a load in flight (a may-analysis: union at joins) to a fixed point.  A register
 leaves the set at the wait's `v_mov_b32 X, R` (inside the asm block that starts with the
 `s_waitcnt`) or at a kernel-final `s_waitcnt vmcnt(0)` asm block.  Any other instruction that
-reads or writes a register in the set is reported.  (The wait counts themselves -- at least N
-vector memory operations issued after each load -- are argued in fs_kernels.hip next to
-row_load.)  Exit status 1 on any finding.
+reads or writes a register in the set is reported.
+
+The same propagation also proves the wait counts.  `s_waitcnt vmcnt(N)` returns once at most N
+vector memory operations are outstanding, and gfx9 retires them in issue order, so a load is
+resident at such a wait only if at least N vector memory instructions (global_ / buffer_ /
+flat_ / scratch_ loads, stores and atomics, LDS-DMA included) were issued after it.  Each
+register in flight carries the MINIMUM count of those over every path that reaches a point
+(min at joins, capped), and a wait whose immediate exceeds the count of a register it copies
+out is reported.  Exit status 1 on any finding.
 """
 import os
 import re
@@ -144,51 +150,130 @@ def blocks(lines):
     return out
 
 
+VMEM = ("global_", "buffer_", "flat_", "scratch_")
+CAP = 1 << 10  # counts saturate here (enough for any wait immediate; keeps loops finite)
+
+
+def is_vmem(mnemonic):
+    return mnemonic.startswith(VMEM)
+
+
+def prune_if_else(bbs):
+    """The two `s_cbranch_execz` skips of one divergent if / else cannot both be taken: the
+    then-part's skip means its mask (exec & cond) was empty, and the else-part then runs with the
+    whole incoming mask, which is not empty (a wave that reaches code has live lanes).  The
+    compiler's form is
+
+        B:  s_and_saveexec_b64 sX, cond ; s_xor_b64 sY, exec, sX ; ... s_cbranch_execz E
+        E:  s_andn2_saveexec_b64 sZ, sY ; s_cbranch_execz J
+            (or s_or_saveexec_b64 sZ, sY ; s_xor_b64 exec, exec, sZ ; s_cbranch_execz J)
+
+    so B's skip edge is redirected to a copy of E without its skip to J.  (Without this, the wait
+    counts would be checked on a path where neither half of env_step's if / else stores.)"""
+    index = {lab: i for i, (lab, _, _) in enumerate(bbs)}
+    extra = []
+    for i, (lab, its, succ) in enumerate(bbs):
+        code = [x for x in its if isinstance(x, str)]
+        if not code or not code[-1].startswith("s_cbranch_execz"):
+            continue
+        tgt = code[-1].split()[1]
+        xor = [x for x in code if x.startswith("s_xor_b64") and ", exec, " in x]
+        if not xor or tgt not in index:
+            continue
+        mask = xor[-1].split()[1].rstrip(",")
+        e_lab, e_its, e_succ = bbs[index[tgt]]
+        e_code = [x for x in e_its if isinstance(x, str)]
+        # the else part opens with s_andn2_saveexec_b64 sZ, sY (exec = sY & ~exec), or with
+        # s_or_saveexec_b64 sZ, sY; s_xor_b64 exec, exec, sZ (exec = sY when the then-part was skipped)
+        if len(e_code) < 2 or not e_code[0].startswith(("s_andn2_saveexec_b64", "s_or_saveexec_b64")) or \
+                e_code[0].split(",")[-1].strip() != mask:
+            continue
+        need_xor = e_code[0].startswith("s_or_saveexec_b64")
+        saved = e_code[0].split()[1].rstrip(",")
+        skip_to = None
+        for x in e_code[1:]:  # instructions that leave exec alone may sit in between
+            if x.startswith("s_cbranch_execz"):
+                skip_to = None if need_xor else x.split()[1]
+                break
+            if x.replace(" ", "") == "s_xor_b64exec,exec," + saved and need_xor:
+                need_xor = False
+                continue
+            if "exec" in x or x.startswith(("s_cbranch", "s_branch", "s_endpgm")):
+                break
+        if skip_to is None:
+            continue
+        copy = e_lab + "#then-skipped"
+        extra.append((copy, e_its, [x for x in e_succ if x != skip_to] or e_succ))
+        bbs[i] = (lab, its, [copy if x == tgt else x for x in succ])
+    return bbs + extra
+
+
 def check_kernel(name, lines):
-    bbs = blocks(lines)
+    bbs = prune_if_else(blocks(lines))
     index = {lab: i for i, (lab, _, _) in enumerate(bbs)}
     if not any(isinstance(it, tuple) and any(x.startswith("global_load") for x in it[1]) for _, its, _ in bbs
                for it in its):
         return None
-    state_in = {lab: set() for lab, _, _ in bbs}
+    # per block entry: {register in flight: min VMEM instructions issued after its load, any path}
+    state_in = {lab: {} for lab, _, _ in bbs}
     findings = set()
     work = [bbs[0][0]]
     seen_once = set()
+
+    def issued(pend):
+        for r in pend:
+            pend[r] = min(CAP, pend[r] + 1)
+
     while work:
         lab = work.pop()
         _, its, succ = bbs[index[lab]]
-        pend = set(state_in[lab])
+        pend = dict(state_in[lab])
         for it in its:
             if isinstance(it, tuple):
                 body = it[1]
                 if body and body[0].startswith("global_load"):
-                    pend |= regs(body[0].split(",")[0])
+                    issued(pend)
+                    for r in regs(body[0].split(",")[0]):
+                        pend[r] = 0
                 elif body and body[0].startswith("s_waitcnt vmcnt"):
-                    if body[0].startswith("s_waitcnt vmcnt(0)") and len(body) == 1:
+                    m = re.match(r"s_waitcnt vmcnt\((\d+)\)", body[0])
+                    need = int(m.group(1)) if m else 0
+                    if need == 0 and len(body) == 1:
                         pend.clear()  # the kernel-final wait
                     for x in body[1:]:
                         p = parse_instr(x)
                         if p and p[0] == "v_mov_b32":
-                            pend -= p[2]
-                            if p[1] & pend:
+                            for r in p[2] & set(pend):
+                                if pend[r] < need:
+                                    findings.add("%s [%s]: vmcnt(%d) copies v%d after only %d vector memory "
+                                                 "instructions on some path: %s" % (name, lab, need, r, pend[r], x))
+                                del pend[r]
+                            if p[1] & set(pend):
                                 findings.add("%s: asm copy writes a register in flight: %s" % (name, x))
                 else:
                     for x in body:
                         p = parse_instr(x)
-                        if p and (p[1] | p[2]) & pend:
+                        if p and (p[1] | p[2]) & set(pend):
                             findings.add("%s: asm touches a register in flight: %s" % (name, x))
+                        if p and is_vmem(p[0]):
+                            issued(pend)
                 continue
             p = parse_instr(it)
             if not p:
                 continue
-            hit = (p[1] | p[2]) & pend
+            hit = (p[1] | p[2]) & set(pend)
             if hit:
                 findings.add("%s [%s]: %s touches in-flight v%s" % (name, lab, it, sorted(hit)))
+            if is_vmem(p[0]):
+                issued(pend)
         for s_ in succ:
             if s_ not in state_in:
                 continue
-            new = state_in[s_] | pend
-            if new != state_in[s_] or s_ not in seen_once:
+            old = state_in[s_]
+            new = dict(old)
+            for r, c in pend.items():
+                new[r] = min(c, new[r]) if r in new else c
+            if new != old or s_ not in seen_once:
                 state_in[s_] = new
                 seen_once.add(s_)
                 work.append(s_)
