@@ -1276,9 +1276,9 @@ __device__ __forceinline__ uint32_t prio_group() {
   return __builtin_amdgcn_s_getreg(4 /* HW_ID */ | (31 << 11)) & 1u;  // bit 0 of the wave slot
 }
 __device__ __forceinline__ void prio_slice(uint32_t grp) {
-  const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
-  if (((now >> kPrioSliceShift) ^ grp) & 1u) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
+  const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime() ^ (grp << kPrioSliceShift);
+  asm volatile("s_bitcmp1_b32 %0, %1\n\ts_cbranch_scc0 .Lprio_lo%=\n\ts_setprio 1\n\ts_branch .Lprio_end%=\n"
+               ".Lprio_lo%=:\n\ts_setprio 0\n.Lprio_end%=:" :: "s"(now), "n"(kPrioSliceShift) : "scc");
 }
 
 // The burst leaves mostly constants in the lane (SetupBattleStart, STAND's ActionInfo).  Where

@@ -26,6 +26,16 @@ def test_kat_actors_gpu(name):
     kat_actors.ALL[name](kat_actors.SimActors)
 
 
+def test_kat_bot_plans_gpu():
+    """The scripted bot's plan logic against the hand-derived restatement of BattleAI.cs
+    (tests/kat_bot.py) through the HIP path: every distance bucket's draw size and outcome map at
+    and around the bucket edges, the TwoHit rules that draw nothing, NoAttack at d > 4 still
+    drawing, every index of every plan (FallBack2's forward "backward dash" included) for P2's bot
+    and for P1's mirrored one, and the decision reading the previous call's FightState."""
+    from tests import kat_bot
+    kat_bot.run(lambda n, p1: kat_bot.SimBot(n, p1))
+
+
 def switch_rounds(sim, ora, rng, rounds, steps, reset_every=0):
     """Lockstep in rounds; between rounds a random subset of arenas switches P2 to the bot and
     another back to the remote actor (mid-episode, pending bursts included), and every
