@@ -14,7 +14,7 @@ INCLUDE = os.path.join(HERE, "..", "include")
 LIB = os.path.join(HERE, "libfootsies.so")
 ARCH = os.environ.get("FOOTSIES_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["fs_kernels.hip", "fs_delay.hip", "fs_gather.hip", "fs_learn.hip", "fs_api.cpp"]
-HEADERS = ["fs_internal.h", "fs_tables.h", "fs_policy.h"]
+HEADERS = ["fs_internal.h", "fs_tables.h", "fs_policy.h", "fs_arena1.h"]
 
 # -ffp-contract=off: no a*b+c fusion -- every float op must round like the C# it restates.
 # -simplifycfg-sink-common=false: SimplifyCFG otherwise sinks the per-branch field stores

@@ -325,8 +325,9 @@ __device__ __forceinline__ void increment_action_frame(Fighter& f, AInfo ai) {
 //   the attack / dash / held direction inputs and the proximity latch.
 // The first two return before the latches are touched (F:263, 285).  Returns whether
 // SetCurrentAction ran; then *rec is the new action's frame-0 record.
-template <bool G>
-__device__ __forceinline__ bool update_action_request(Fighter& f, const InputEval& e, AInfo ai, uint32_t* rec) {
+// The request table entry a fighter reads this tick (`keep`: hasWon or an early return, which
+// leave the guard latches alone) ...
+__device__ __forceinline__ uint32_t request_sel(const Fighter& f, const InputEval& e, AInfo ai, bool& keep) {
   // (take_rsv = rsv set & no stun; take_buf = !take_rsv & buf set & (hit or whiff-cancel) & no stun,
   // as bitwise ops: the short-circuit form materializes each condition as a 0 / 1 word)
   const int rsv = f.rsv, buf = f.buf;
@@ -341,9 +342,12 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   // lanes that differ in action but not in inputs read different LDS banks)
   const uint32_t in8 = ((9u * cls + 3u * e.atk + e.dash) << 3) | (e.held << 1) | (uint32_t)f.prox;
   const uint32_t idx = ((uint32_t)f.act << 8) | (in8 ^ (uint32_t)f.act);
-  const uint32_t sel = won ? (uint32_t)kReqWin + 3u * (uint32_t)f.act + cls
-                           : (early ? (uint32_t)(kReqEarly + a0) : idx);
-  const uint32_t q = tabs<G>().req_table[sel];
+  keep = early | won;
+  return won ? (uint32_t)kReqWin + 3u * (uint32_t)f.act + cls : (early ? (uint32_t)(kReqEarly + a0) : idx);
+}
+// ... and what the entry q does to it.  Returns whether SetCurrentAction ran; then *rec is the new
+// action's frame-0 record.
+__device__ __forceinline__ bool apply_request(Fighter& f, uint32_t q, bool keep, const InputEval& e, uint32_t* rec) {
   const bool set = ((q >> 11) & 1u) != 0;  // SetCurrentAction ran (F:546-563)
   const bool bset = ((q >> 10) & 1u) != 0;
   f.act = set ? (int)(q & 31u) : f.act;
@@ -351,11 +355,16 @@ __device__ __forceinline__ bool update_action_request(Fighter& f, const InputEva
   f.frame = set ? 0 : f.frame;
   f.hits = set ? 0 : f.hits;
   f.rsv = set ? NONE : f.rsv;
-  const bool keep = early | won;
   f.in_back = keep ? f.in_back : (e.held & 1u);  // for proximity guard (F:263)
   f.prox = keep ? f.prox : 0u;                   // F:285
   *rec = (q >> 12) & 255u;
   return set;
+}
+template <bool G>
+__device__ __forceinline__ bool update_action_request(Fighter& f, const InputEval& e, AInfo ai, uint32_t* rec) {
+  bool keep;
+  const uint32_t sel = request_sel(f, e, ai, keep);
+  return apply_request(f, tabs<G>().req_table[sel], keep, e, rec);
 }
 
 // UpdateMovement (F:291-319).  FORWARD / BACKWARD walk at the fighter speeds, any other action
@@ -1182,10 +1191,12 @@ __device__ __forceinline__ void reset_burst(Lane& L, bool after_ko, const Actors
 // ---------------------------------------------------------------------------
 // Stores at a 32-bit byte offset from a kernel-argument base: the address is one SGPR pair plus
 // one VGPR (global_store ... saddr), with no 64-bit address arithmetic per store.  The host
-// splits launches so every trajectory offset fits (fs_api.cpp, kMaxLaunchRows).
+// splits launches so every trajectory offset fits (fs_api.cpp, kMaxLaunchRows).  The outputs
+// stream out and are not read back by the launch, so the stores are non-temporal (`nt`): they
+// do not pile up as dirty lines in L2 (1000-tick launches +4.8 %, 20-tick +2.4 %, A/B on one box).
 template <class T>
 __device__ __forceinline__ void st_off(T* base, uint32_t byte_off, T v) {
-  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = v;
+  __builtin_nontemporal_store(v, reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off));
 }
 
 __device__ __forceinline__ void write_obs(const Lane& L, uint8_t* guard, uint8_t* move, float* move_frame,
@@ -1818,10 +1829,37 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
   store_arena(A, st, i);
 }
 
+#include "fs_arena1.h"
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 static inline dim3 grid_for(int n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+// Which kernel runs a fused launch with action rows.  The two-lane kernel needs two waves per SIMD
+// to hide its LDS round trips, and has them from 32 768 arenas on; the one-lane kernel issues ~18 %
+// fewer instructions per arena-tick but needs twice the arenas for the same waves: with one wave
+// per SIMD (65 536 arenas, C3) it exposes the tick's dependent LDS reads and runs 16-18 % slower;
+// from two waves per SIMD (131 072 arenas) on it matches the two-lane kernel with a remote P2 and
+// beats it by 12-25 % with the scripted bot.  So the one-lane kernel takes the
+// launches with at least two of its waves per SIMD.  FOOTSIES_FUSED_LANES=1 / 2 forces one kernel
+// (A/B timing, and the parity suite runs both).
+static int simd_count() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;  // MI355X
+  return 4 * cus;
+}
+static bool fused_one_lane(int n_envs) {
+  static const int forced = [] {
+    const char* e = getenv("FOOTSIES_FUSED_LANES");
+    return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+  }();
+  if (forced) return forced == 1;
+  static const int threshold = 2 * 64 * simd_count();
+  return n_envs >= threshold;
+}
 
 template <int FM, int P2>
 static void launch_step_p2(const StepParams& p, hipStream_t s) {
@@ -1829,7 +1867,12 @@ static void launch_step_p2(const StepParams& p, hipStream_t s) {
   if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
   else if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
-  else hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
+  else if constexpr (P2 != kActors) {
+    if (fused_one_lane(p.n_envs)) hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
+    else hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
+  } else {
+    hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
+  }
 }
 
 template <int FM>

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of built libfootsies.so variants on the GPU (measurement only).
 
-  python tools/ab_time.py LIB [LIB ...] [--rounds R] [--envs N] [--ticks T]
+  python tools/ab_time.py LIB[@VAR=VALUE,...] [LIB ...] [--rounds R] [--envs N] [--ticks T]
 
 Each library is timed in its own subprocess (FOOTSIES_LIB override), rounds interleaved so
 box-level drift hits every variant alike.  Per library and P2 mode (external = C3, bot = C2):
@@ -73,7 +73,11 @@ def main():
     times = {lib: [] for lib in a.libs}
     for r in range(a.rounds):
         for lib in a.libs:
-            env = dict(os.environ, FOOTSIES_LIB=os.path.abspath(lib))
+            # LIB[@VAR=VALUE,...]: the same library under a different environment (e.g.
+            # FOOTSIES_FUSED_LANES=2 for the two-lane fused kernel)
+            path, _, extra = lib.partition("@")
+            env = dict(os.environ, FOOTSIES_LIB=os.path.abspath(path))
+            env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             line = [x for x in p.stdout.splitlines() if x.startswith("RESULT")]
             if p.returncode or not line:

@@ -83,7 +83,8 @@ def parse_instr(line):
 
 
 def kernels(asm):
-    """{name: [lines]} for every kernel function in the assembly."""
+    """{name: [lines]} for every kernel function in the assembly: from its label to its
+    .Lfunc_end label (a kernel can hold several s_endpgm, e.g. an early exit of idle lanes)."""
     out, cur, name = {}, None, None
     for line in asm.splitlines():
         m = re.match(r"^(_Z\S+):\s*;", line)
@@ -92,8 +93,7 @@ def kernels(asm):
             out[name] = cur
             continue
         if cur is not None:
-            if line.strip().startswith("s_endpgm"):
-                cur.append(line)
+            if line.startswith(".Lfunc_end"):
                 cur = None
                 continue
             cur.append(line)
@@ -159,52 +159,65 @@ def is_vmem(mnemonic):
 
 
 def prune_if_else(bbs):
-    """The two `s_cbranch_execz` skips of one divergent if / else cannot both be taken: the
-    then-part's skip means its mask (exec & cond) was empty, and the else-part then runs with the
-    whole incoming mask, which is not empty (a wave that reaches code has live lanes).  The
-    compiler's form is
+    """The two exec-mask skips of one divergent if / else cannot both be taken: the then-part's
+    skip means its mask (exec & cond) was empty, and the else-part then runs with the whole
+    incoming mask, which is not empty (a wave that reaches code has live lanes).  The compiler's
+    forms are
 
         B:  s_and_saveexec_b64 sX, cond ; s_xor_b64 sY, exec, sX ; ... s_cbranch_execz E
-        E:  s_andn2_saveexec_b64 sZ, sY ; s_cbranch_execz J
-            (or s_or_saveexec_b64 sZ, sY ; s_xor_b64 exec, exec, sZ ; s_cbranch_execz J)
+            (or s_cbranch_execnz T, the then-part elsewhere, falling through to E when empty)
+        E:  s_andn2_saveexec_b64 sZ, sY ; s_cbranch_execz J      (or s_cbranch_execnz X, else-part
+            (or s_or_saveexec_b64 sZ, sY ; s_xor_b64 exec, exec, sZ ; s_cbranch_execz J)   elsewhere)
 
-    so B's skip edge is redirected to a copy of E without its skip to J.  (Without this, the wait
-    counts would be checked on a path where neither half of env_step's if / else stores.)"""
+    so B's then-empty edge is redirected to a copy of E without its else-empty edge.  (Without
+    this, the wait counts would be checked on a path where neither half of env_step's if / else
+    stores.)"""
     index = {lab: i for i, (lab, _, _) in enumerate(bbs)}
     extra = []
     for i, (lab, its, succ) in enumerate(bbs):
         code = [x for x in its if isinstance(x, str)]
-        if not code or not code[-1].startswith("s_cbranch_execz"):
+        if not code or not code[-1].startswith(("s_cbranch_execz", "s_cbranch_execnz")):
             continue
-        tgt = code[-1].split()[1]
         xor = [x for x in code if x.startswith("s_xor_b64") and ", exec, " in x]
-        if not xor or tgt not in index:
+        if not xor:
+            continue
+        if code[-1].startswith("s_cbranch_execz"):
+            e_lab = code[-1].split()[1]  # the taken edge: the then-part was empty
+        else:
+            e_lab = bbs[i + 1][0] if i + 1 < len(bbs) else None  # the fall-through edge
+        if e_lab not in index:
             continue
         mask = xor[-1].split()[1].rstrip(",")
-        e_lab, e_its, e_succ = bbs[index[tgt]]
+        _, e_its, e_succ = bbs[index[e_lab]]
         e_code = [x for x in e_its if isinstance(x, str)]
-        # the else part opens with s_andn2_saveexec_b64 sZ, sY (exec = sY & ~exec), or with
-        # s_or_saveexec_b64 sZ, sY; s_xor_b64 exec, exec, sZ (exec = sY when the then-part was skipped)
+        # the else header: s_andn2_saveexec_b64 sZ, sY (exec = sY & ~exec), or s_or_saveexec_b64
+        # sZ, sY; s_xor_b64 exec, exec, sZ (exec = sY when the then-part was skipped)
         if len(e_code) < 2 or not e_code[0].startswith(("s_andn2_saveexec_b64", "s_or_saveexec_b64")) or \
                 e_code[0].split(",")[-1].strip() != mask:
             continue
         need_xor = e_code[0].startswith("s_or_saveexec_b64")
         saved = e_code[0].split()[1].rstrip(",")
-        skip_to = None
+        empty_to = None
         for x in e_code[1:]:  # instructions that leave exec alone may sit in between
-            if x.startswith("s_cbranch_execz"):
-                skip_to = None if need_xor else x.split()[1]
+            if x.startswith(("s_cbranch_execz", "s_cbranch_execnz")):
+                if not need_xor:
+                    if x.startswith("s_cbranch_execz"):
+                        empty_to = x.split()[1]
+                    else:  # taken when the else mask is live: empty falls through
+                        k = index[e_lab]
+                        empty_to = bbs[k + 1][0] if k + 1 < len(bbs) else None
                 break
             if x.replace(" ", "") == "s_xor_b64exec,exec," + saved and need_xor:
                 need_xor = False
                 continue
             if "exec" in x or x.startswith(("s_cbranch", "s_branch", "s_endpgm")):
                 break
-        if skip_to is None:
+        if empty_to is None:
             continue
         copy = e_lab + "#then-skipped"
-        extra.append((copy, e_its, [x for x in e_succ if x != skip_to] or e_succ))
-        bbs[i] = (lab, its, [copy if x == tgt else x for x in succ])
+        if copy not in index and all(c[0] != copy for c in extra):
+            extra.append((copy, e_its, [x for x in e_succ if x != empty_to] or e_succ))
+        bbs[i] = (lab, its, [copy if x == e_lab else x for x in succ])
     return bbs + extra
 
 

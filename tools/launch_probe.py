@@ -66,6 +66,13 @@ for j in range(R):
 res["region_us"] = 1e6 * statistics.median(walls)
 res["region_us_min"] = 1e6 * min(walls)
 res["host_call_us"] = 1e6 * statistics.median(host)
+abi = L.fs_abi_version
+xs = []
+for _ in range(R):
+    t = time.perf_counter()
+    abi()
+    xs.append(time.perf_counter() - t)
+res["ctypes_trivial_call_us"] = 1e6 * statistics.median(xs)
 s = sim.stream
 torch.cuda.synchronize(dev)
 with torch.cuda.stream(s):
@@ -93,7 +100,9 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "launch_probe.json"))
     a = ap.parse_args()
     cases = {"default": ({}, 0), "side_stream": ({}, 1), "no_interrupt": ({"HSA_ENABLE_INTERRUPT": "0"}, 0),
-             "no_interrupt_side": ({"HSA_ENABLE_INTERRUPT": "0"}, 1)}
+             "no_interrupt_side": ({"HSA_ENABLE_INTERRUPT": "0"}, 1),
+             "dev_kernarg": ({"HIP_FORCE_DEV_KERNARG": "1"}, 0),
+             "host_kernarg": ({"HIP_FORCE_DEV_KERNARG": "0"}, 0)}
     out = {"envs": a.envs, "ticks": a.ticks, "reps": a.reps, "cases": {}}
     for r in range(a.rounds):
         for name, (env, side) in cases.items():
