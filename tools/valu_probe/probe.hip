@@ -73,6 +73,21 @@ __global__ __launch_bounds__(256) void k_probe(int iters, unsigned long long* cy
       asm volatile(REP8("v_bfe_u32 %0, %0, 1, 30\n v_bfe_u32 %1, %1, 1, 30\n v_bfe_u32 %2, %2, 1, 30\n "
                         "v_bfe_u32 %3, %3, 1, 30\n")
                    : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if constexpr (KIND == 12) {  // vcc written by SALU, then 32 e32 cndmasks
+      const unsigned k = s0 | 1u;
+      asm volatile("s_mov_b64 vcc, exec\n" REP8("v_cndmask_b32 %0, %0, %4, vcc\n v_cndmask_b32 %1, %1, %4, vcc\n "
+                                                "v_cndmask_b32 %2, %2, %4, vcc\n v_cndmask_b32 %3, %3, %4, vcc\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(k) : "vcc");
+    } else if constexpr (KIND == 13) {  // one v_cmp, then 128 e32 cndmasks (counted as 4 blocks)
+      const unsigned k = s0 | 1u;
+      asm volatile("v_cmp_gt_u32 vcc, %0, %1\n" REP4(REP8("v_cndmask_b32 %0, %0, %4, vcc\n v_cndmask_b32 %1, %1, %4, vcc\n "
+                                                          "v_cndmask_b32 %2, %2, %4, vcc\n v_cndmask_b32 %3, %3, %4, vcc\n"))
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(k) : "vcc");
+    } else if constexpr (KIND == 14) {  // e32 cndmask reading vcc, with 3 v_add between each (is it the read?)
+      const unsigned k = s0 | 1u;
+      asm volatile("v_cmp_gt_u32 vcc, %0, %1\n" REP8("v_cndmask_b32 %0, %0, %4, vcc\n v_add_u32 %1, 1, %1\n "
+                                                     "v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(k) : "vcc");
     } else {  // 24 VALU + 8 SALU per block of 32
       asm volatile(REP8("v_add_u32 %0, 1, %0\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n s_add_u32 %4, %4, 1\n")
                    : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0) : : "scc");
@@ -85,7 +100,7 @@ __global__ __launch_bounds__(256) void k_probe(int iters, unsigned long long* cy
 }
 
 template <int KIND>
-static void run(const char* name, int cus, int waves_per_simd, int iters, bool first) {
+static void run(const char* name, int cus, int waves_per_simd, int iters, bool first, int per_block = 32) {
   const int blocks = cus * waves_per_simd;  // 256 threads = 4 waves = one per SIMD of a CU
   const int waves = blocks * 4;
   unsigned long long* cyc;
@@ -107,7 +122,7 @@ static void run(const char* name, int cus, int waves_per_simd, int iters, bool f
   hipMemcpy(h.data(), cyc, waves * sizeof(unsigned long long), hipMemcpyDeviceToHost);
   unsigned long long mx = 0, sum = 0;
   for (auto v : h) { mx = v > mx ? v : mx; sum += v; }
-  const double per_wave = (double)iters * 32;
+  const double per_wave = (double)iters * per_block;
   // per SIMD: waves_per_simd x per_wave instructions in (about) the slowest wave's cycles
   printf("%s{\"kind\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_instr_per_wave\": %.3f, "
          "\"simd_cycles_per_instr\": %.3f, \"simd_instr_per_cycle\": %.3f, \"kernel_ms\": %.3f, "
@@ -139,6 +154,9 @@ int main() {
     run<9>("v_cmp_gt_u32 vcc", cus, w, iters, first);
     run<10>("v_and_b32 / v_lshlrev_b32", cus, w, iters, first);
     run<11>("v_bfe_u32", cus, w, iters, first);
+    run<12>("v_cndmask_b32 vcc from s_mov", cus, w, iters, first);
+    run<13>("v_cndmask_b32 x128 per v_cmp", cus, w, iters / 4, first, 128);
+    run<14>("1 v_cndmask_b32 + 3 v_add_u32", cus, w, iters, first);
   }
   printf("]}\n");
   return 0;
