@@ -304,13 +304,19 @@ def pmc_traffic(kernel, envs, ticks):
 
 
 def issue_profile(kernel, envs, ticks):
-    """The step kernel's instruction-issue picture from the committed SQ counter summary
-    (profiles/*_sq.json, tools/pmc_table.py --json over tools/prof_pmc.sh passes of the same
-    kernel at the same arena count): instructions issued per wave-tick and wave cycles per
-    wave-tick (quad-cycles) and the quad-cycles parked in s_waitcnt; `frac` = one wave's issued
-    instructions over its quad-cycles, the share of its issue ceiling (one instruction per wave
-    per 4 cycles) it uses.  Reported beside the HBM roofline: this kernel is bound by each wave's
-    instruction stream and its LDS waits, not by bytes.  None when no summary matches."""
+    """The step kernel's instruction-issue picture, per wave and per SIMD, from committed summaries
+    of the same kernel at the same arena count:
+    * profiles/*_sq.json (tools/pmc_table.py --json over tools/prof_pmc.sh passes): instructions
+      and VALU issued per wave-tick, wave cycles per wave-tick (quad-cycles) and the quad-cycles
+      parked in s_waitcnt; `wave_frac` = one wave's issued instructions over its quad-cycles;
+    * profiles/*_issue_model.json (tools/issue_model.py): the SIMD level.  `issue_frac` = the
+      kernel's env-step rate at its own occupancy (2 waves per SIMD at 65 536 arenas) over the
+      plateau the same kernel reaches at 4 and 8 waves per SIMD (tools/occupancy_sweep.sh), where
+      only the SIMDs' issue is near its limit: the share of the SIMD issue rate this instruction
+      stream can use that it does use.  Beside it the VALU pipe time priced by
+      tools/valu_probe's per-class SIMD costs (plain 32-bit ops 2.4 cycles at 2 waves, VOP3-only /
+      DPP / VOPC / SGPR-operand kinds 4.7-5.6), an estimate (the probe shows the costs do not add).
+    None when no SQ summary matches."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))):
@@ -320,17 +326,27 @@ def issue_profile(kernel, envs, ticks):
         for k in kernels if isinstance(kernels, list) else []:  # (other summaries have other layouts)
             if isinstance(k, dict) and k.get("kernel") == kernel and k.get("envs") == envs:
                 pw = k["per_wave_tick"]
-                best = {"bound": "each wave's own instruction issue (one instruction per wave per 4 cycles, "
-                                 "MI355X_MICROARCH.md constants table) and its exposed LDS waits (DESIGN.md section 5)",
-                        "insts_per_wave_tick": round(k["insts_per_wave_tick"], 1),
+                best = {"insts_per_wave_tick": round(k["insts_per_wave_tick"], 1),
                         "valu_per_wave_tick": round(pw.get("SQ_INSTS_VALU", 0.0), 1),
                         "salu_per_wave_tick": round(pw.get("SQ_INSTS_SALU", 0.0), 1),
                         "wave_quad_cycles_per_wave_tick": round(pw.get("SQ_WAVE_CYCLES", 0.0), 1),
                         "wait_quad_cycles_per_wave_tick": round(pw.get("SQ_WAIT_ANY", 0.0), 1),
                         "waves_per_simd": k.get("waves", 0) / MI355X_SIMDS,
-                        # instructions issued over the wave's quad-cycles: its issue ceiling in use
-                        "frac": k["wave_issue_frac"], "ticks_per_launch_profiled": k["ticks_per_launch"],
+                        # instructions issued over the wave's quad-cycles: one wave's issue ceiling in use
+                        "wave_frac": k["wave_issue_frac"], "ticks_per_launch_profiled": k["ticks_per_launch"],
                         "source": os.path.relpath(path, ROOT)}
+    if best is None:
+        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_issue_model.json"))):
+        with open(path) as f:
+            m = json.load(f)
+        if isinstance(m, dict) and m.get("kernel") == kernel and m.get("envs") == envs:
+            best.update({"issue_frac": m.get("issue_frac"),
+                         "rate_by_waves_per_simd": m.get("rate_by_waves_per_simd"),
+                         "valu_pipe_frac_priced": m["valu_pipe_frac_priced"],
+                         "valu_pipe_frac_if_all_fast": m["valu_pipe_frac_if_all_fast"],
+                         "simd_cycles_per_valu_class": m["simd_cycles_per_valu"],
+                         "model_source": os.path.relpath(path, ROOT)})
     return best
 
 
@@ -584,6 +600,11 @@ def main():
         kname = "fsk::k_step<0, 0>"
     achieved = bytes_per_launch / kt / 1e9
     tr = pmc_traffic(kname, N, ticks)
+    issue = issue_profile(kname, N, ticks)
+    # what binds the kernel: its SIMDs' instruction issue when the committed issue model puts the
+    # kernel nearer that limit than HBM's (the C3 kernel: 0.90 of its issue plateau, ~0.3 of HBM)
+    hbm_frac = achieved / HBM_PEAK_GBPS
+    bound = "simd-issue" if issue and (issue.get("issue_frac") or 0.0) > hbm_frac else "hbm"
     other = "step" if args.mode == "fused" else "fused"
     out = {
         "metric": METRIC,
@@ -610,12 +631,16 @@ def main():
         "timing": {"regions": R, "region_walls_ms": res[args.mode]["region_walls_ms"],
                    "note": "each region times exactly `steps` steps between barrier + synchronize pairs "
                            "(host wall clock, max over ranks); value = the median region"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "roofline": {"bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": tr[0] if tr else None,
                      "traffic_source": tr[1] if tr else None,
                      "kernel": kname, "ticks_per_launch": ticks, "avg_launch_us": kt * 1e6,
                      "median_launch_us": kmed * 1e6, "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "issue": issue_profile(kname, N, ticks)},
+                     "note": "achieved / peak / frac: the HBM roofline of the kernel's algorithmic bytes; `bound` "
+                             "names what binds it: the SIMDs' instruction issue (issue.issue_frac, the rate over the "
+                             "same kernel's plateau at 4-8 waves per SIMD) when a SIMD-level issue model of this "
+                             "kernel is committed",
+                     "issue": issue},
         "kernel_at_timed_shape": {"ticks_per_launch": chunk if args.mode == "fused" else 1,
                                   "avg_launch_us": st_kt * 1e6, "median_launch_us": st_kmed * 1e6,
                                   "algorithmic_bytes_per_launch": st_bytes,

@@ -88,6 +88,36 @@ __global__ __launch_bounds__(256) void k_probe(int iters, unsigned long long* cy
       asm volatile("v_cmp_gt_u32 vcc, %0, %1\n" REP8("v_cndmask_b32 %0, %0, %4, vcc\n v_add_u32 %1, 1, %1\n "
                                                      "v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n")
                    : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(k) : "vcc");
+    } else if constexpr (KIND == 15) {  // the VOP3 (8-byte) encoding of a plain add: encoding or operation?
+      asm volatile(REP8("v_add_u32_e64 %0, %0, 1\n v_add_u32_e64 %1, %1, 1\n v_add_u32_e64 %2, %2, 1\n "
+                        "v_add_u32_e64 %3, %3, 1\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if constexpr (KIND == 16) {  // VOP2 with the constant in an SGPR (4 bytes) instead of a literal
+      const unsigned m = __builtin_amdgcn_readfirstlane(s0 | 0x7fff0000u);
+      asm volatile(REP8("v_and_b32 %0, %4, %0\n v_xor_b32 %1, %4, %1\n v_and_b32 %2, %4, %2\n v_xor_b32 %3, %4, %3\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(m));
+    } else if constexpr (KIND == 17) {  // pairs of vcc cndmasks between plain adds
+      const unsigned k = s0 | 1u;
+      asm volatile("v_cmp_gt_u32 vcc, %0, %1\n" REP8("v_cndmask_b32 %0, %0, %4, vcc\n v_cndmask_b32 %1, %1, %4, vcc\n "
+                                                     "v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(k) : "vcc");
+    } else if constexpr (KIND == 18) {  // VOPC in its VOP3 form, into SGPR pairs (no vcc)
+      unsigned long long m0, m1, m2, m3;
+      asm volatile(REP8("v_cmp_gt_u32_e64 %4, %0, %1\n v_cmp_gt_u32_e64 %5, %1, %2\n v_cmp_gt_u32_e64 %6, %2, %3\n "
+                        "v_cmp_gt_u32_e64 %7, %3, %0\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=s"(m0), "=s"(m1), "=s"(m2), "=s"(m3));
+    } else if constexpr (KIND == 19) {  // v_mov_b32 of a literal (8 bytes)
+      asm volatile(REP8("v_mov_b32 %0, 0x12345\n v_mov_b32 %1, 0x23456\n v_mov_b32 %2, 0x34567\n v_mov_b32 %3, 0x45678\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if constexpr (KIND == 20) {  // one v_cmp into vcc, then 3 plain adds
+      asm volatile(REP8("v_cmp_gt_u32 vcc, %0, %1\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : : "vcc");
+    } else if constexpr (KIND == 21) {  // one v_and with a literal, then 3 plain adds
+      asm volatile(REP8("v_and_b32 %0, 0x7fffffff, %0\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if constexpr (KIND == 22) {  // one VOP3 (v_bfe_u32), then 3 plain adds
+      asm volatile(REP8("v_bfe_u32 %0, %0, 1, 30\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n")
+                   : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
     } else {  // 24 VALU + 8 SALU per block of 32
       asm volatile(REP8("v_add_u32 %0, 1, %0\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n s_add_u32 %4, %4, 1\n")
                    : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0) : : "scc");
@@ -157,6 +187,14 @@ int main() {
     run<12>("v_cndmask_b32 vcc from s_mov", cus, w, iters, first);
     run<13>("v_cndmask_b32 x128 per v_cmp", cus, w, iters / 4, first, 128);
     run<14>("1 v_cndmask_b32 + 3 v_add_u32", cus, w, iters, first);
+    run<15>("v_add_u32_e64 (VOP3 encoding)", cus, w, iters, first);
+    run<16>("v_and / v_xor with an SGPR constant", cus, w, iters, first);
+    run<17>("2 v_cndmask_b32 vcc + 2 v_add_u32", cus, w, iters, first);
+    run<18>("v_cmp_gt_u32_e64 into SGPR pairs", cus, w, iters, first);
+    run<19>("v_mov_b32 literal", cus, w, iters, first);
+    run<20>("1 v_cmp vcc + 3 v_add_u32", cus, w, iters, first);
+    run<21>("1 v_and literal + 3 v_add_u32", cus, w, iters, first);
+    run<22>("1 v_bfe_u32 + 3 v_add_u32", cus, w, iters, first);
   }
   printf("]}\n");
   return 0;
