@@ -4,15 +4,18 @@
 // fused into one kernel per network, fp32 throughout.  The torch learner of ppo.py defines the
 // values (its loss and autograd's gradients); tests/test_gpu_learn.py compares the two.
 //
-// One wave per block, 32 samples per tile (kTile), a grid-stride loop over tiles.  The per-sample
-// phases run lane = sample with the small weights (W1, W3: 2 KB each) as wave-uniform scalar
-// operands; everything touching the 64 x 64 W2 runs lane = hidden unit with W2's row or column
-// in registers, looping over the tile's samples whose vectors are broadcast rows of an LDS stage:
-//  1 (sample) h1 = tanh(W1 x + b1), staged;      2 (unit j) h2[s][j] = tanh(W2[j] . h1[s] + b2[j]);
-//  3 (sample) output, loss gradient g3 (staged), g2 = (W3^T g3)(1 - h2^2);
-//  4 (unit j) dW3[.][j] += g3[s] h2[s][j];       g2 then replaces h2 in the stage;
-//  5 (unit i) g1 = (W2^T g2)[i] (1 - h1[i]^2), lane i's rows of dW2 (g2[s][i] h1[s]) and dW1.
-// The gradients accumulate in registers across tiles.
+// One wave per block, 32 samples per tile (kTile), a grid-stride loop over tiles.  Every GEMM runs
+// on fp32 MFMA with the tile's activations as rows of an LDS stage (h1, then g1; h2, then g2):
+//  1 h1 = tanh(W1 x + b1) and 2 h2 = tanh(W2 h1 + b2) (32 x 32 x 2, hidden units on the rows);
+//  3 the actor's logits W3 h2 + b3 (16 x 16 x 4, 8 of 16 rows used) exchanged between lane halves,
+//    then (lane = sample) the loss and its gradient g3 (staged); the critic's value on VALU;
+//  4 (lane = unit j) dW3[.][j] += g3[s] h2[s][j];
+//  5 g2 = (W3^T g3)(1 - h2^2) (actor: 32 x 32 x 2, K = 8) over h2 in place;
+//  6 dW2 += G2^T H1 and 7 g1 = (W2^T g2)(1 - h1^2) over h1 in place, W2^T read as rows from a copy
+//    k_ppo_t64 writes per call; 8 (lane = unit i) dW1 and db1.
+// The gradients accumulate in registers across tiles.  On gfx950 the fp32 MFMA shares the SIMD
+// with the VALU (tools/mfma_probe/rate.hip: ~140 TFLOP/s device-wide, and MFMA and VALU time add
+// up in the ablations), so the tile time is the sum of the two, not their max.
 // Each wave writes its partial gradient to the workspace; k_ppo_reduce sums the partials in a
 // fixed order, so the result does not depend on scheduling.  Nothing here is integer game
 // state: this is the learner beside the simulator, not part of the bit-exact path.
@@ -30,7 +33,8 @@ constexpr int kPad = kH + 4;   // LDS row stride of the h1 / h2 stages (b128 wri
 #define FSL_TILE 32  // 32-sample tiles: a 19 KB stage, so two waves per SIMD fit the LDS
 #endif
 constexpr int kTile = FSL_TILE;  // samples per tile (lanes >= kTile idle in the per-sample phases)
-constexpr int kMaxWaves = 65536 / kTile;  // grid cap: 1024 (64-sample tiles) or 2048 waves
+constexpr int kMaxWaves = 65536 / kTile;
+static_assert(kTile == 32, "the output layer's MFMA maps (16 x 16 column blocks, 32 x 32 results) assume 32-sample tiles");  // grid cap: 1024 (64-sample tiles) or 2048 waves
 
 template <int OUT>
 constexpr int n_params() { return kH * kF + kH + kH * kH + kH + OUT * kH + OUT; }
@@ -60,6 +64,10 @@ typedef float F16 __attribute__((ext_vector_type(16)));  // a 32 x 32 f32 MFMA a
 __device__ __forceinline__ F16 mfma32(float a, float b, F16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
+typedef float F4 __attribute__((ext_vector_type(4)));  // a 16 x 16 f32 MFMA accumulator
+__device__ __forceinline__ F4 mfma16(float a, float b, F4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 // tanh without branches (the library tanhf runs both of its branches under divergence, ~30
 // instructions): |x| < 0.625 the same odd polynomial, above it 1 - 2 / (2^(2|x| log2 e) + 1)
 // with the hardware exp2 and reciprocal (within a few ulp of tanhf; 2^+inf -> 1 exactly).
@@ -74,6 +82,48 @@ __device__ __forceinline__ float tanh_fast(float x) {
   p = fmaf(x2, p, -0.3333328068256378f);                              // 0xbeaaaa99
   const float small = fmaf(x2, ax * p, ax);
   return copysignf(ax < 0.625f ? small : big, x);
+}
+
+// PPO's actor loss of one sample (ppo.py update) from its logits z: log_softmax, the clipped
+// surrogate and the entropy bonus; g3 = d loss / d z (zero for padding rows, !valid).
+__device__ __forceinline__ void actor_loss(const float (&z)[8], const float (&tail)[4], bool valid, const Coef& c,
+                                           float (&g3)[8], float& pg_sum, float& ent_sum) {
+  float m = z[0];
+#pragma unroll
+  for (int o = 1; o < 8; ++o) m = fmaxf(m, z[o]);
+  float se = 0.f;
+#pragma unroll
+  for (int o = 0; o < 8; ++o) se += expf(z[o] - m);
+  const float lse = m + logf(se);
+  float lp[8], p[8];
+  const int act = (int)tail[0];
+  float lp_a = 0.f, ent = 0.f;
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    lp[o] = z[o] - lse;
+    p[o] = expf(lp[o]);
+    lp_a = o == act ? lp[o] : lp_a;
+    ent -= p[o] * lp[o];
+  }
+  const float adv = tail[2];
+  const float rt = expf(lp_a - tail[1]);
+  const float s1 = rt * adv, rc = fminf(fmaxf(rt, 1.f - c.clip), 1.f + c.clip), s2 = rc * adv;
+  // torch.min's gradient goes to the smaller operand (half to each on a tie); clamp's passes
+  // inside [1 - clip, 1 + clip]
+  const float inr = (rt >= 1.f - c.clip && rt <= 1.f + c.clip) ? 1.f : 0.f;
+  const float wsel = s1 < s2 ? 1.f : (s1 > s2 ? inr : 0.5f + 0.5f * inr);
+  const float g_lpa = -(adv * wsel) * c.inv_n * rt;
+  const float g_ent = c.ent_coef * c.inv_n;  // d(-ent_coef mean H) / d(exp(lp) lp) per term
+  float g_lp[8], gsum = 0.f;
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    g_lp[o] = (o == act ? g_lpa : 0.f) + g_ent * (p[o] * lp[o] + p[o]);
+    gsum += g_lp[o];
+  }
+#pragma unroll
+  for (int o = 0; o < 8; ++o) g3[o] = valid ? g_lp[o] - p[o] * gsum : 0.f;  // log_softmax backward
+  pg_sum += valid ? -fminf(s1, s2) : 0.f;
+  ent_sum += valid ? ent : 0.f;
 }
 
 // Accumulator element q of lane (r, hf) is row (q & 3) + 8 (q >> 2) + 4 hf, column r: four runs
@@ -117,7 +167,8 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
                                                          const float* __restrict__ w2, const float* __restrict__ b2,
                                                          const float* __restrict__ w3, const float* __restrict__ b3,
                                                          Coef c, float* __restrict__ partial,
-                                                         const uint8_t* __restrict__ actions = nullptr) {
+                                                         const uint8_t* __restrict__ actions = nullptr,
+                                                         const float* __restrict__ w2t = nullptr) {
   constexpr int kStride = EVAL ? kF : kRow;
   __shared__ float sX[kTile][kF];
   __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample, then g1
@@ -138,8 +189,8 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     // weights re-read every tile (L1 / scalar-cache hits): hoisted out of the loop they would
     // hold ~200 registers; W3 / B3 as wave-uniform scalar loads (constant address space)
-    const float *w1v = w1, *b1v = b1, *w2v = w2, *b2v = b2, *w3v = w3, *b3v = b3;
-    asm volatile("" : "+s"(w1v), "+s"(b1v), "+s"(w2v), "+s"(b2v), "+s"(w3v), "+s"(b3v));
+    const float *w1v = w1, *b1v = b1, *w2v = w2, *b2v = b2, *w3v = w3, *b3v = b3, *w2tv = w2t;
+    asm volatile("" : "+s"(w1v), "+s"(b1v), "+s"(w2v), "+s"(b2v), "+s"(w3v), "+s"(b3v), "+s"(w2tv));
     const CPtr W3 = (CPtr)w3v, B3 = (CPtr)b3v;
     const int64_t left = n - tile * kTile;
     const int ns = (int)(left < kTile ? left : kTile);
@@ -242,82 +293,69 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       continue;
     }
 
-    // ---- (lane = sample) the output, the loss gradient g3 and g2 = (W3^T g3)(1 - h2^2) ---------
-    float g2[kH];
-    if (lane < kTile) {
+    // ---- the output layer and the loss gradient g3 (staged in sG3) ---------------------------
+    if constexpr (OUT == 8) {
+      // Z^T[o][s] = b3[o] + W3[o] . h2[s] on MFMA 16 x 16 x 4: rows o (8 of 16 used), columns the
+      // 16 samples of block nb, K = 64 as 16 steps of k = 16 q + t; lane (c, q) = (lane & 15,
+      // lane >> 4) supplies A = W3[c][16 q + t] and B = H2[16 nb + c][16 q + t] and holds rows
+      // 4 q .. 4 q + 3 of column c.
+      const int c16 = lane & 15, q4 = lane >> 4;
+      float wz[16];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = c16 < 8 ? *reinterpret_cast<const float4*>(&w3v[c16 * kH + 16 * q4 + 4 * u])
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        wz[4 * u] = v.x; wz[4 * u + 1] = v.y; wz[4 * u + 2] = v.z; wz[4 * u + 3] = v.w;
+      }
+      const float4 bz = q4 < 2 ? *reinterpret_cast<const float4*>(&b3v[4 * q4]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      F4 zacc[2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        float hz[16];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 v = *reinterpret_cast<const float4*>(&sH2[16 * nb + c16][16 * q4 + 4 * u]);
+          hz[4 * u] = v.x; hz[4 * u + 1] = v.y; hz[4 * u + 2] = v.z; hz[4 * u + 3] = v.w;
+        }
+        F4 acc = {bz.x, bz.y, bz.z, bz.w};
+#pragma unroll
+        for (int t = 0; t < 16; ++t) acc = mfma16(wz[t], hz[t], acc);
+        zacc[nb] = acc;
+      }
+      // lane s < 32 (block nb = s >> 4 = q) holds z[s][4 nb ..]; lane s ^ 16 holds z[s][4 (1 - nb) ..]
+      const F4 own = q4 & 1 ? zacc[1] : zacc[0], snd = q4 & 1 ? zacc[0] : zacc[1];
+      F4 rcv;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) rcv[v] = __shfl_xor(snd[v], 16, 64);
+      if (lane < kTile) {
+        float z[8], g3[8];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          z[v] = q4 ? rcv[v] : own[v];
+          z[4 + v] = q4 ? own[v] : rcv[v];
+        }
+        actor_loss(z, tail, valid, c, g3, pg_sum, ent_sum);
+#pragma unroll
+        for (int o = 0; o < 8; ++o) dB3[o] += g3[o];
+        *reinterpret_cast<float4*>(&sG3[lane][0]) = make_float4(g3[0], g3[1], g3[2], g3[3]);
+        *reinterpret_cast<float4*>(&sG3[lane][4]) = make_float4(g3[4], g3[5], g3[6], g3[7]);
+      }
+    } else if (lane < kTile) {  // the critic (lane = sample): v = W3 . h2 + b3, the value loss
+      float h2[kH];
 #pragma unroll
       for (int k = 0; k < kH; k += 4) {
         const float4 v = *reinterpret_cast<const float4*>(&sH2[lane][k]);
-        g2[k] = v.x; g2[k + 1] = v.y; g2[k + 2] = v.z; g2[k + 3] = v.w;  // h2 for now
+        h2[k] = v.x; h2[k + 1] = v.y; h2[k + 2] = v.z; h2[k + 3] = v.w;
       }
-      float g3[8];
-      if constexpr (OUT == 8) {
-        float z[8];
+      float v = B3[0];
 #pragma unroll
-        for (int o = 0; o < 8; ++o) {
-          float a = B3[o];
-#pragma unroll
-          for (int j = 0; j < kH; ++j) a = fmaf(W3[o * kH + j], g2[j], a);
-          z[o] = a;
-        }
-        // log_softmax, then the clipped surrogate and the entropy bonus (ppo.py update)
-        float m = z[0];
-#pragma unroll
-        for (int o = 1; o < 8; ++o) m = fmaxf(m, z[o]);
-        float se = 0.f;
-#pragma unroll
-        for (int o = 0; o < 8; ++o) se += expf(z[o] - m);
-        const float lse = m + logf(se);
-        float lp[8], p[8];
-        const int act = (int)tail[0];
-        float lp_a = 0.f, ent = 0.f;
-#pragma unroll
-        for (int o = 0; o < 8; ++o) {
-          lp[o] = z[o] - lse;
-          p[o] = expf(lp[o]);
-          lp_a = o == act ? lp[o] : lp_a;
-          ent -= p[o] * lp[o];
-        }
-        const float adv = tail[2];
-        const float rt = expf(lp_a - tail[1]);
-        const float s1 = rt * adv, rc = fminf(fmaxf(rt, 1.f - c.clip), 1.f + c.clip), s2 = rc * adv;
-        // torch.min's gradient goes to the smaller operand (half to each on a tie); clamp's passes
-        // inside [1 - clip, 1 + clip]
-        const float inr = (rt >= 1.f - c.clip && rt <= 1.f + c.clip) ? 1.f : 0.f;
-        const float wsel = s1 < s2 ? 1.f : (s1 > s2 ? inr : 0.5f + 0.5f * inr);
-        const float g_lpa = -(adv * wsel) * c.inv_n * rt;
-        const float g_ent = c.ent_coef * c.inv_n;  // d(-ent_coef mean H) / d(exp(lp) lp) per term
-        float g_lp[8], gsum = 0.f;
-#pragma unroll
-        for (int o = 0; o < 8; ++o) {
-          g_lp[o] = (o == act ? g_lpa : 0.f) + g_ent * (p[o] * lp[o] + p[o]);
-          gsum += g_lp[o];
-        }
-#pragma unroll
-        for (int o = 0; o < 8; ++o) g3[o] = valid ? g_lp[o] - p[o] * gsum : 0.f;  // log_softmax backward
-        pg_sum += valid ? -fminf(s1, s2) : 0.f;
-        ent_sum += valid ? ent : 0.f;
-      } else {
-        float v = B3[0];
-#pragma unroll
-        for (int j = 0; j < kH; ++j) v = fmaf(W3[j], g2[j], v);
-        const float d = v - tail[3];
-        g3[0] = valid ? 2.f * d * (c.vf_coef * c.inv_n) : 0.f;
-        vf_sum += valid ? d * d : 0.f;
-#pragma unroll
-        for (int o = 1; o < 8; ++o) g3[o] = 0.f;
-      }
-#pragma unroll
-      for (int o = 0; o < OUT; ++o) dB3[o] += g3[o];
-      *reinterpret_cast<float4*>(&sG3[lane][0]) = make_float4(g3[0], g3[1], g3[2], g3[3]);
-      *reinterpret_cast<float4*>(&sG3[lane][4]) = make_float4(g3[4], g3[5], g3[6], g3[7]);
-#pragma unroll
-      for (int j = 0; j < kH; ++j) {
-        float gh = 0.f;
-#pragma unroll
-        for (int o = 0; o < OUT; ++o) gh = fmaf(W3[o * kH + j], g3[o], gh);
-        g2[j] = gh * (1.f - g2[j] * g2[j]);  // tanh backward
-      }
+      for (int j = 0; j < kH; ++j) v = fmaf(W3[j], h2[j], v);
+      const float d = v - tail[3];
+      const float g3 = valid ? 2.f * d * (c.vf_coef * c.inv_n) : 0.f;
+      vf_sum += valid ? d * d : 0.f;
+      dB3[0] += g3;
+      *reinterpret_cast<float4*>(&sG3[lane][0]) = make_float4(g3, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(&sG3[lane][4]) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
 
@@ -328,10 +366,42 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       for (int o = 0; o < OUT; ++o) dW3[o] = fmaf(sG3[t][o], h2c, dW3[o]);
     }
     __syncthreads();
-    if (lane < kTile) {  // g2 replaces h2 in its stage
+    if constexpr (OUT == 8) {
+      // g2 = (W3^T g3)(1 - h2^2) on MFMA 32 x 32 x 2, K = the 8 outputs as 4 steps of (o = t, t + 4):
+      // A = W3[t + 4 hf][32 jb + r], B = G3[r][t + 4 hf]; the result overwrites h2 in place (each
+      // lane rewrites only the stage entries it read)
+      const float4 gq = *reinterpret_cast<const float4*>(&sG3[r][4 * hf]);
+      const float gb[4] = {gq.x, gq.y, gq.z, gq.w};
 #pragma unroll
-      for (int k = 0; k < kH; k += 4)
-        *reinterpret_cast<float4*>(&sH2[lane][k]) = make_float4(g2[k], g2[k + 1], g2[k + 2], g2[k + 3]);
+      for (int jb = 0; jb < 2; ++jb) {
+        F16 acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc = mfma32(w3v[(t + 4 * hf) * kH + 32 * jb + r], gb[t], acc);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          float4* hp = reinterpret_cast<float4*>(&sH2[r][32 * jb + 8 * qq + 4 * hf]);
+          const float4 hv = *hp;
+          *hp = make_float4(acc[4 * qq] * (1.f - hv.x * hv.x), acc[4 * qq + 1] * (1.f - hv.y * hv.y),
+                            acc[4 * qq + 2] * (1.f - hv.z * hv.z), acc[4 * qq + 3] * (1.f - hv.w * hv.w));
+        }
+      }
+    } else {
+      // the critic's g2 = (W3^T g3)(1 - h2^2) = (W3[j] g3[s])(1 - h2^2), in place in the same
+      // layout: lane (r, hf) rewrites sample r's units 32 jb + 8 qq + 4 hf .. + 3
+      const float g3 = sG3[r][0];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int j = 32 * jb + 8 * qq + 4 * hf;
+          const float4 w = *reinterpret_cast<const float4*>(&w3v[j]);
+          float4* hp = reinterpret_cast<float4*>(&sH2[r][j]);
+          const float4 hv = *hp;
+          *hp = make_float4(fmaf(w.x, g3, 0.f) * (1.f - hv.x * hv.x), fmaf(w.y, g3, 0.f) * (1.f - hv.y * hv.y),
+                            fmaf(w.z, g3, 0.f) * (1.f - hv.z * hv.z), fmaf(w.w, g3, 0.f) * (1.f - hv.w * hv.w));
+        }
     }
     __syncthreads();
 
@@ -362,9 +432,12 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       }
 #pragma unroll 1
       for (int ib = 0; ib < 2; ++ib) {
-        float wa[32];
+        float wa[32];  // W2's column 32 ib + r = row 32 ib + r of W2^T (k_ppo_t64), as float4s
 #pragma unroll
-        for (int t = 0; t < 32; ++t) wa[t] = w2v[(t + 32 * hf) * kH + 32 * ib + r];
+        for (int u = 0; u < 8; ++u) {
+          const float4 v = *reinterpret_cast<const float4*>(&w2tv[(32 * ib + r) * kH + 32 * hf + 4 * u]);
+          wa[4 * u] = v.x; wa[4 * u + 1] = v.y; wa[4 * u + 2] = v.z; wa[4 * u + 3] = v.w;
+        }
         F16 acc;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
@@ -432,6 +505,19 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     out[n_params<OUT>() + 0] = pg_sum;
     out[n_params<OUT>() + 1] = vf_sum;
     out[n_params<OUT>() + 2] = ent_sum;
+  }
+}
+
+// W2^T of both networks into the workspace (64 x 64 each), so the backward pass through W2 reads
+// its A operand (a column of W2 per lane) as row vectors, like the forward pass.  The values
+// are copied, not recomputed: the products and their order are unchanged.
+__global__ __launch_bounds__(256) void k_ppo_t64(const float* __restrict__ wa, const float* __restrict__ wc,
+                                                float* __restrict__ out) {
+  const float* w = blockIdx.y ? wc : wa;
+  float* o = out + blockIdx.y * kH * kH;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < kH * kH; e += gridDim.x * 256) {
+    const int i = e >> 6, j = e & 63;  // out[i][j] = w[j][i]
+    o[e] = w[j * kH + i];
   }
 }
 
@@ -545,7 +631,8 @@ hipError_t launch_ppo_pack(const float* x, const uint8_t* act, const float* old,
 }
 
 size_t ppo_workspace_bytes() {
-  return sizeof(float) * (size_t)fsl::kMaxWaves * (fsl::partial_stride<8>() + fsl::partial_stride<1>());
+  return sizeof(float) * ((size_t)fsl::kMaxWaves * (fsl::partial_stride<8>() + fsl::partial_stride<1>()) +
+                          2 * fsl::kH * fsl::kH);
 }
 
 hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
@@ -557,12 +644,14 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
   const Coef c{clip, vf_coef, ent_coef, 1.0f / (float)n};
   float* pa = static_cast<float*>(workspace);
   float* pc = pa + (size_t)kMaxWaves * partial_stride<8>();
+  float* w2t = pc + (size_t)kMaxWaves * partial_stride<1>();  // [2][64][64]: actor, critic
   hipError_t e = hipMemsetAsync(loss, 0, 3 * sizeof(float), s);
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ppo_t64, dim3(4, 2), dim3(256), 0, s, actor[2], critic[2], w2t);
   hipLaunchKernelGGL(k_ppo_grad<8>, dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1], actor[2],
-                     actor[3], actor[4], actor[5], c, pa);
+                     actor[3], actor[4], actor[5], c, pa, nullptr, w2t);
   hipLaunchKernelGGL(k_ppo_grad<1>, dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1], critic[2],
-                     critic[3], critic[4], critic[5], c, pc);
+                     critic[3], critic[4], critic[5], c, pc, nullptr, w2t + kH * kH);
   hipLaunchKernelGGL(k_ppo_reduce<8>, dim3((n_params<8>() + 3 + 63) / 64), dim3(1024), 0, s, pa, waves, grad, loss,
                      c.inv_n);
   hipLaunchKernelGGL(k_ppo_reduce<1>, dim3((n_params<1>() + 3 + 63) / 64), dim3(1024), 0, s, pc, waves,
