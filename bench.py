@@ -412,7 +412,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; the modulo only matters when ranks are rehearsed on fewer devices
     local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # a process group whenever a launcher started the ranks, a single one included (the driver's
+    # torch.distributed.run at N = 1, or tests/test_gpu_rccl.py): RCCL then carries the barrier,
+    # the max-over-ranks and the gather modes at every N
+    grouped = world > 1 or "WORLD_SIZE" in os.environ
+    if grouped:
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -469,7 +473,7 @@ def main():
     base1, base2 = p1.data_ptr(), p2.data_ptr()
 
     def barrier():
-        if world > 1:
+        if grouped:
             dist.barrier()
 
     def timed(fn, k0, n):
@@ -484,7 +488,7 @@ def main():
         wall = time.perf_counter() - t0
         local_walls.append(wall)
         t = torch.tensor([wall], dtype=torch.float64, device=coll_dev)
-        if world > 1:
+        if grouped:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -557,7 +561,7 @@ def main():
             rc = rc or fs_pack(h, C.c_void_p(rec.data_ptr()))
             if rc:
                 check(rc, h)
-            if world > 1 and args.dist_backend == "nccl":
+            if grouped and args.dist_backend == "nccl":
                 dist.all_gather_into_tensor(gbuf, rec)
     gwall = timed(run_step_gather, W, kg)
 
@@ -568,7 +572,7 @@ def main():
             rc = rc or fs_pack(h, C.c_void_p(rec.data_ptr()))
             if rc:
                 check(rc, h)
-            if world > 1 and args.dist_backend == "nccl":
+            if grouped and args.dist_backend == "nccl":
                 gather_records_to(rec, 0)
     grwall = timed(run_step_gather_root, W, kg)
     # The dominant kernel of the reported mode, back-to-back launches.  The roofline block is
@@ -623,8 +627,8 @@ def main():
                                 "C3: %d arenas/GPU" % N) + ", self-play random actions, P2 external, auto-reset same-step",
                    "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
                    "ticks_per_launch": chunk if args.mode == "fused" else 1, "parallelism": "arena-shard x%d" % world},
-        "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,
-                  "backend": dist.get_backend() if world > 1 else None,
+        "ranks": {"world_size": dist.get_world_size() if grouped else 1,
+                  "backend": dist.get_backend() if grouped else None,
                   "rank_walls_ms": res[args.mode]["rank_walls_ms"],
                   "note": "world_size / backend as the process group reports them (nccl = RCCL); each rank's "
                           "median region wall, before the max over ranks"},
@@ -653,7 +657,8 @@ def main():
         "step_gather_mode": {"value": world * N * kg / gwall, "ms_per_step": 1e3 * gwall / kg, "steps": kg,
                              "bytes_gathered_per_step": world * N * _abi.FS_RECORD_BYTES,
                              "note": "fs_step + fs_pack_outputs + one all_gather_into_tensor of the 40-B "
-                                     "(obs, reward, done) records over RCCL per step (none at 1 GPU or with --dist-backend gloo)"},
+                                     "(obs, reward, done) records over RCCL per step (none without a process group -- a plain "
+                                     "1-GPU run -- or with --dist-backend gloo)"},
         "step_gather_root_mode": {"value": world * N * kg / grwall, "ms_per_step": 1e3 * grwall / kg, "steps": kg,
                                   "bytes_into_rank0_per_step": (world - 1) * N * _abi.FS_RECORD_BYTES,
                                   "note": "fs_step + fs_pack_outputs + the records of every rank gathered to rank 0 "
@@ -686,7 +691,7 @@ def main():
     if rank == 0:
         print(json.dumps(out))
     sim.close()
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 
