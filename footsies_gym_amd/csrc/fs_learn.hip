@@ -13,9 +13,10 @@
 //  5 g2 = (W3^T g3)(1 - h2^2) (actor: 32 x 32 x 2, K = 8) over h2 in place;
 //  6 dW2 += G2^T H1 and 7 g1 = (W2^T g2)(1 - h1^2) over h1 in place, W2^T read as rows from a copy
 //    k_ppo_t64 writes per call; 8 (lane = unit i) dW1 and db1.
-// The gradients accumulate in registers across tiles.  On gfx950 the fp32 MFMA shares the SIMD
-// with the VALU (tools/mfma_probe/rate.hip: ~140 TFLOP/s device-wide, and MFMA and VALU time add
-// up in the ablations), so the tile time is the sum of the two, not their max.
+// The gradients accumulate in registers across tiles.  On gfx950 a SIMD does not issue VALU
+// while an MFMA executes, not even another wave's (tools/mfma_probe/overlap.hip), so the tile
+// time is the sum of the MFMA time (64 cycles per 32x32x2, tools/mfma_probe/rate.hip) and the
+// VALU time, not their max.
 // Each wave writes its partial gradient to the workspace; k_ppo_reduce sums the partials in a
 // fixed order, so the result does not depend on scheduling.  Nothing here is integer game
 // state: this is the learner beside the simulator, not part of the bit-exact path.
