@@ -30,12 +30,10 @@ constexpr int kF = 8;          // features
 constexpr int kH = 64;         // hidden units
 constexpr int kRow = 12;       // rows: x[8], action, old log-prob, advantage, return
 constexpr int kPad = kH + 4;   // LDS row stride of the h1 / h2 stages (b128 writes spread over banks)
-#ifndef FSL_TILE
-#define FSL_TILE 32  // 32-sample tiles: a 19 KB stage, so two waves per SIMD fit the LDS
-#endif
-constexpr int kTile = FSL_TILE;  // samples per tile (lanes >= kTile idle in the per-sample phases)
-constexpr int kMaxWaves = 65536 / kTile;
-static_assert(kTile == 32, "the output layer's MFMA maps (16 x 16 column blocks, 32 x 32 results) assume 32-sample tiles");  // grid cap: 1024 (64-sample tiles) or 2048 waves
+// 32 samples per tile: a 19 KB stage, so two waves per SIMD fit the LDS; the MFMA maps (32 x 32
+// results, the output layer's two 16-column blocks) are written for it
+constexpr int kTile = 32;        // (lanes >= kTile idle in the per-sample phases)
+constexpr int kMaxWaves = 2048;  // grid cap: two waves per SIMD
 
 template <int OUT>
 constexpr int n_params() { return kH * kF + kH + kH * kH + kH + OUT * kH + OUT; }
@@ -46,9 +44,6 @@ constexpr int partial_stride() { return (n_params<OUT>() + 3 + 3) & ~3; }  // + 
 constexpr int kOffB1 = kH * kF, kOffW2 = kOffB1 + kH, kOffB2 = kOffW2 + kH * kH, kOffW3 = kOffB2 + kH;
 template <int OUT>
 constexpr int off_b3() { return kOffW3 + OUT * kH; }
-
-typedef float F2 __attribute__((ext_vector_type(2)));  // packed f32 pair (v_pk_fma_f32)
-__device__ __forceinline__ F2 fma2(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 using CPtr = const __attribute__((address_space(4))) float*;  // scalar (constant) loads
 
