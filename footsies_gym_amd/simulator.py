@@ -44,13 +44,11 @@ def encode_actions(actions):
     raise ValueError("actions must be (N,3) booleans or (N,) ints, got shape %s" % (a.shape,))
 
 
-# (left, right, attack) of every uint8 input code: one gather decodes a whole batch
-_ACTION_BOOLS = np.array([[(c & 1) != 0, (c & 2) != 0, (c & 4) != 0] for c in range(256)], dtype=bool)
-
-
 def decode_actions(bits):
-    """uint8 3-bit inputs -> (N,3) booleans (FootsiesState.__post_init__, state.py:26-36)."""
-    return _ACTION_BOOLS[np.asarray(bits, dtype=np.uint8)]
+    """uint8 3-bit inputs -> (N,3) booleans (FootsiesState.__post_init__, state.py:26-36).  Three
+    bit tests stacked: a (256, 3) table gathered with the codes measured 5x slower in numpy."""
+    b = np.asarray(bits, dtype=np.uint8)
+    return np.stack([(b & 1) != 0, (b & 2) != 0, (b & 4) != 0], axis=-1)
 
 
 class FootsiesSim:
