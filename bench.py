@@ -502,22 +502,36 @@ def main():
         return [round(1e3 * float(e.item()), 4) for e in every]
 
     def kernel_time(fn, lo, hi, launches, ticks_per_launch):
-        """Average kernel duration with the queue pre-filled (a spin kernel holds the GPU while
-        the host enqueues), so event pairs bracket back-to-back kernels, not host gaps.  Every
+        """The kernel's launch-to-launch period with the queue pre-filled (a spin kernel holds the
+        GPU while the host enqueues, so no host gap is timed): (average, median).  The average is
+        one event pair around `launches` back-to-back launches; the median comes from a second
+        pass with an event pair around each launch, whose records themselves add a few
+        microseconds between kernels (measured: 27 vs 24 us at 20 ticks per launch).  Every
         launch reads action rows inside [lo, hi)."""
+        def spin():
+            try:
+                torch.cuda._sleep(int(2e7))
+            except Exception:
+                pass
+        start = lambda j: lo + (j * ticks_per_launch) % max(1, hi - lo - ticks_per_launch + 1)  # noqa: E731
         torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        spin()
+        e0.record()
+        for j in range(launches):
+            fn(start(j), ticks_per_launch)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        avg = e0.elapsed_time(e1) / 1e3 / launches
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
-        try:
-            torch.cuda._sleep(int(2e7))
-        except Exception:
-            pass
+        spin()
         for j, (a, b) in enumerate(evs):
             a.record()
-            fn(lo + (j * ticks_per_launch) % max(1, hi - lo - ticks_per_launch + 1), ticks_per_launch)
+            fn(start(j), ticks_per_launch)
             b.record()
         torch.cuda.synchronize(dev)
         d = sorted(a.elapsed_time(b) / 1e3 for a, b in evs)
-        return sum(d) / len(d), d[len(d) // 2]
+        return avg, d[len(d) // 2]
 
     # warm-up (untimed)
     if W:
@@ -640,7 +654,7 @@ def main():
                      "traffic_source": tr[1] if tr else None,
                      "kernel": kname, "ticks_per_launch": ticks, "avg_launch_us": kt * 1e6,
                      "median_launch_us": kmed * 1e6, "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "note": "achieved / peak / frac: the HBM roofline of the kernel's algorithmic bytes; `bound` "
+                     "note": "avg_launch_us: back-to-back launch period (one HIP event pair over the launches), median_launch_us: per-launch event pairs (their records add a few us between kernels); achieved / peak / frac: the HBM roofline of the kernel's algorithmic bytes; `bound` "
                              "names what binds it: the SIMDs' instruction issue (issue.issue_frac, the rate over the "
                              "same kernel's plateau at 4-8 waves per SIMD) when a SIMD-level issue model of this "
                              "kernel is committed",
