@@ -1,7 +1,9 @@
 """The driver-shaped bench region in a fresh process (measurement tool): 5 warm-up ticks, then 5
 regions of one 20-tick fs_step_n launch between synchronizes, optionally after a GPU spin
-(torch.cuda._sleep) and / or a host spin, to see whether the first regions pay a cold start.
-Usage on the GPU box: python tools/cold_region_probe.py none|gpu_spin|host_spin|both"""
+(torch.cuda._sleep) and / or a host spin, to see whether the first regions pay a cold start;
+or after many launches: 3000 one-element torch kernels (torch_launches) or 3000 one-tick
+fs_step_n launches (sim_launches) on the same stream.
+Usage on the GPU box: python tools/cold_region_probe.py none|gpu_spin|host_spin|both|torch_launches|sim_launches"""
 import ctypes as C, json, sys, time, os
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -28,6 +30,15 @@ if variant in ("host_spin", "both"):
     t = time.perf_counter()
     while time.perf_counter() - t < 0.05:
         pass
+if variant == "torch_launches":
+    x = torch.zeros(1, device=dev)
+    for _ in range(3000):
+        x.add_(1)
+    torch.cuda.synchronize(dev)
+if variant == "sim_launches":
+    for j in range(3000):
+        assert fs_step_n(h, 1, C.c_void_p(b1 + (j % T) * N), C.c_void_p(b2 + (j % T) * N), 0, C.byref(td)) == 0
+    torch.cuda.synchronize(dev)
 walls = []
 for r in range(R):
     k = W + r * T
