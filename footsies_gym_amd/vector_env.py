@@ -348,11 +348,33 @@ class FootsiesEnv(_EnvBase):
         self._most_recent_observation, self._most_recent_info = dict(o), dict(i)
         return o, i
 
+    @staticmethod
+    def _py_host(h):
+        """_py of the one arena straight from the host copy of the outputs (the values that
+        step_result_from_outputs + _py produce, without the batch arrays in between)."""
+        def pos(x):
+            return float(str(np.float32(x)))
+        g, m, mf, p = h["guard"][0].tolist(), h["move"][0].tolist(), h["move_frame"][0].tolist(), h["position"][0].tolist()
+        a1, a2 = h["action"][0].tolist()
+        hs = h["hitstun"][0].tolist()
+        o = {"guard": (g[0], g[1]), "move": (m[0], m[1]), "move_frame": (int(mf[0]), int(mf[1])),
+             "position": (pos(p[0]), pos(p[1]))}
+        i = {"frame": int(h["frame"][0]), "p1_action": (a1 & 1 != 0, a1 & 2 != 0, a1 & 4 != 0),
+             "p2_action": (a2 & 1 != 0, a2 & 2 != 0, a2 & 4 != 0), "p1_hitstun": hs[0], "p2_hitstun": hs[1], **o}
+        return o, i
+
     def step(self, action):
-        obs, rew, term, trunc, info = self.venv.step(np.asarray([action]).reshape(1, 3))
-        o, i = self._py(obs, info)
+        # the one-arena path of FootsiesVectorEnv.step (next-step auto-reset: no final_* outputs),
+        # converted from the host buffer directly (tests/test_gpu_api.py holds it to the batch path)
+        v = self.venv
+        v._check_open()
+        p2 = v._p2_actions()
+        v.sim.step(None if v.by_example else np.asarray([action]).reshape(1, 3), p2)
+        h = v.sim.outputs_numpy(copy=False)
+        o, i = self._py_host(h)
+        v._last = (o, i)  # (the wrapped opponent reads this env's most recent dicts, not these)
         self._most_recent_observation, self._most_recent_info = dict(o), dict(i)
-        return o, float(rew[0]), bool(term[0]), False, i
+        return o, float(h["reward"][0]), bool(h["terminated"][0]), False, i
 
     def close(self):
         self.venv.close()

@@ -548,3 +548,41 @@ def test_single_env_after_close_raises_game_closed_error():
         env.step((False, False, True))
     with pytest.raises(FootsiesGameClosedError):
         env.reset()
+
+
+@pytest.mark.parametrize("opponent", [None, "callable"])
+def test_single_env_step_equals_one_arena_vector_env(opponent):
+    """FootsiesEnv.step (its direct host conversion) == FootsiesVectorEnv(1, next-step auto-reset)
+    through the batch path, step for step over terminations, with the bot or a remote P2."""
+    from footsies_gym_amd.simulator import encode_actions
+    from footsies_gym_amd.vector_env import FootsiesEnv, FootsiesVectorEnv
+    seen = []
+
+    def opp(obs, info):  # reads the agent's most recent single-arena dicts (FE:525-527)
+        seen.append(obs["position"])
+        return (False, obs["position"][0] < 0, True)
+    single = FootsiesEnv(seed=3, opponent=None if opponent is None else opp)
+
+    def batch_opp(obs, info):  # the same P2 policy over the batch env's own (obs, info)
+        return np.array([encode_actions([opp(*FootsiesEnv._py(obs, info))])[0]], np.uint8)
+    wrapped = None if opponent is None else batch_opp
+    venv = FootsiesVectorEnv(1, seed=3, autoreset_mode="next_step", opponent=wrapped)
+    rng = np.random.default_rng(5)
+    o1, i1 = single.reset(seed=3)
+    o2, i2 = FootsiesEnv._py(*venv.reset(seed=3))
+    assert (o1, i1) == (o2, i2)
+    dones = 0
+    for t in range(3000):
+        a = tuple(bool(b) for b in rng.integers(0, 2, 3))
+        o1, r1, d1, tr1, i1 = single.step(a)
+        obs, rew, term, trunc, info = venv.step(np.asarray([a]).reshape(1, 3))
+        o2, i2 = FootsiesEnv._py(obs, info)
+        assert (o1, r1, d1, tr1, i1) == (o2, float(rew[0]), bool(term[0]), False, i2), t
+        if d1:
+            dones += 1
+            assert single.reset() == FootsiesEnv._py(*venv.reset())
+    assert dones > 0
+    if opponent is not None:
+        assert seen
+    single.close()
+    venv.close()

@@ -238,3 +238,24 @@ def test_battle_state_load_rejects_airborne_or_flipped_fighters():
     ok = json.loads(B.dumps(doc))
     ok["p1State"]["position"] = [-2.0, -0.0]
     B.load_into(st.copy(), 0, json.dumps(ok))
+
+
+def test_single_env_host_conversion_equals_batch_path():
+    """FootsiesEnv.step's direct conversion of the one arena's host outputs (_py_host) gives the
+    dicts, values and Python types of the batch path (step_result_from_outputs + _py)."""
+    from footsies_gym_amd.vector_env import FootsiesEnv, step_result_from_outputs
+    rng = np.random.default_rng(0)
+
+    def types(d):
+        return {k: tuple(type(x) for x in v) if isinstance(v, tuple) else type(v) for k, v in d.items()}
+    for _ in range(500):
+        h = {"guard": rng.integers(0, 4, (1, 2)).astype(np.uint8), "move": rng.integers(0, 17, (1, 2)).astype(np.uint8),
+             "move_frame": rng.integers(0, 60, (1, 2)).astype(np.float32),
+             "position": (rng.standard_normal((1, 2)) * 3).astype(np.float32),
+             "action": rng.integers(0, 8, (1, 2)).astype(np.uint8), "hitstun": rng.integers(0, 30, (1, 2)).astype(np.uint8),
+             "frame": rng.integers(-1, 3000, (1,)).astype(np.int32), "reward": rng.standard_normal(1),
+             "terminated": rng.integers(0, 2, 1).astype(np.uint8), "truncated": np.zeros(1, np.uint8)}
+        obs, _, _, _, info = step_result_from_outputs(h, "next_step")
+        (o1, i1), (o2, i2) = FootsiesEnv._py(obs, info), FootsiesEnv._py_host(h)
+        assert o1 == o2 and i1 == i2 and list(i1) == list(i2)
+        assert types(o1) == types(o2) and types(i1) == types(i2)
