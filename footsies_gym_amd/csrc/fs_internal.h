@@ -85,7 +85,12 @@ struct StepParams {
   int p1_bot;     // kActors: P1 is the bot (FS_P1_BOT)
   int p2_resets;  // kActors: P2's bot is Reset at Intro (the handle was created with FS_P2_BOT)
   int p2_noop;    // kActors: a non-bot P2 presses nothing (FS_P2_NOOP handle)
+  // host actions of a one-tick launch over at most kInlineArenas arenas, carried in the kernel
+  // arguments instead of a staging copy (inl_n != 0): byte a of inl[player] is arena a's input
+  int inl_n;
+  uint32_t inl[2][8];
 };
+constexpr int kInlineArenas = 32;  // sizeof(StepParams::inl[0])
 
 struct ResetParams {
   DevState st;

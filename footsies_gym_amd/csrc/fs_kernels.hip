@@ -1471,8 +1471,13 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   const bool reads = k == 0 ? (!POL && !(P2 == kActors && p.p1_bot)) : p2_rows;
   auto fetch = [&](int t) -> uint32_t {
     if (!reads) return 0u;
-    if constexpr (HASH) return hash_action(p.action_seed, p.arena_base + (uint64_t)a, p.t0 + (uint64_t)t, k);
-    else return src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a];
+    if constexpr (HASH) {
+      return hash_action(p.action_seed, p.arena_base + (uint64_t)a, p.t0 + (uint64_t)t, k);
+    } else {
+      if (!FUSED && p.inl_n)  // host inputs carried in the kernel arguments (fs_api.cpp)
+        return (p.inl[k][(uint32_t)a >> 2] >> (8u * ((uint32_t)a & 3u))) & 0xffu;
+      return src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a];
+    }
   };
   // the arena state and the first action are in flight while the block stages the tables
   Lane L;

@@ -49,6 +49,15 @@ def test_lockstep_random(oracle_lib, p2):
     run_lockstep(sim, ora, 600, np.random.default_rng(1), sticky=0.0)
 
 
+@pytest.mark.parametrize("n", [1, 7, 32, 33])
+@pytest.mark.parametrize("p2", ["external", "bot"])
+def test_lockstep_few_arenas_host_actions(oracle_lib, n, p2):
+    """Host actions of at most 32 arenas travel in the kernel arguments (no staging copy); 33
+    takes the staging path.  Both lockstep with the oracle, terminals and resets included."""
+    sim, ora = make_pair(oracle_lib, n, p2, seed=3 + n)
+    run_lockstep(sim, ora, 2500, np.random.default_rng(n), state_every=250, sticky=0.5)
+
+
 @pytest.mark.parametrize("p2", ["external", "bot"])
 def test_lockstep_sticky(oracle_lib, p2):
     sim, ora = make_pair(oracle_lib, 512, p2, seed=5)
