@@ -59,7 +59,8 @@ class FootsiesSim:
     """
 
     def __init__(self, num_envs, device=0, p2_mode="bot", dense_reward=True, float_mode="strict",
-                 autoreset_mode="same_step", seed=0, frame_delay=0, p1_mode="external", arena_base=0):
+                 autoreset_mode="same_step", seed=0, frame_delay=0, p1_mode="external", arena_base=0,
+                 host_outputs=False):
         torch = _torch()
         if not torch.cuda.is_available():
             raise RuntimeError("FootsiesSim needs a HIP device (torch.cuda.is_available() is False)")
@@ -96,8 +97,16 @@ class FootsiesSim:
             nbytes = n * cols * np.dtype(dt).itemsize
             layout.append((name, dt, shape, total, nbytes))
             total += (nbytes + 255) // 256 * 256
-        with torch.cuda.device(self.device):
-            self._out_buf = torch.zeros(total, dtype=torch.uint8, device=self.device)
+        # host_outputs: the bound buffers are pinned host memory, which the kernels write across
+        # the bus; a step's outputs are then on the host once the stream is done, with no copy
+        # (the single-arena drop-in, where the copy's own latency was a third of a step).
+        # outputs() then returns host tensors.
+        self.host_outputs = bool(host_outputs)
+        if self.host_outputs:
+            self._out_buf = torch.zeros(total, dtype=torch.uint8, pin_memory=True)
+        else:
+            with torch.cuda.device(self.device):
+                self._out_buf = torch.zeros(total, dtype=torch.uint8, device=self.device)
         for name, dt, shape, off, nbytes in layout:
             self._out[name] = self._out_buf[off:off + nbytes].view(getattr(torch, _TORCH_DTYPES[dt])).view(shape)
         self._out_layout = layout
@@ -109,7 +118,9 @@ class FootsiesSim:
         for name in _abi.OUTPUT_SPEC:
             t = self._out[name]
             _copy_device(t.data_ptr(), getattr(own, name), t.numel() * t.element_size())
-        bind = _abi.fs_outputs(**{name: t.data_ptr() for name, t in self._out.items()})
+        # (pinned host buffers are bound through their device-side address, hipHostGetDevicePointer)
+        base = _host_device_pointer(self._out_buf.data_ptr()) if self.host_outputs else self._out_buf.data_ptr()
+        bind = _abi.fs_outputs(**{name: base + off for name, _, _, off, _ in layout})
         check(lib().fs_bind_outputs(h, C.byref(bind)), h)
         self.use_torch_stream()
 
@@ -239,15 +250,19 @@ class FootsiesSim:
         buffer.  copy=False returns views of that buffer, overwritten by the next call."""
         torch = _torch()
         if self._host_buf is None:
-            self._host_buf = torch.empty(self._out_buf.numel(), dtype=torch.uint8, pin_memory=True)
+            self._host_buf = (self._out_buf if self.host_outputs else
+                              torch.empty(self._out_buf.numel(), dtype=torch.uint8, pin_memory=True))
             host = self._host_buf.numpy()
             # the typed views of the pinned buffer, made once (building them costs ~20 us a call)
             self._host_views = {name: host[off:off + nbytes].view(dt).reshape(shape)
                                 for name, dt, shape, off, nbytes in self._out_layout}
-        # on the handle's own stream, so the copy is ordered after the library's kernels whatever
-        # torch's current stream is (a blocking copy: it returns once the bytes are on the host)
-        with torch.cuda.stream(self._stream):
-            self._host_buf.copy_(self._out_buf)
+        if self.host_outputs:  # the kernels wrote them there: wait for the handle's stream
+            check(lib().fs_sync(self._h), self._h)
+        else:
+            # on the handle's own stream, so the copy is ordered after the library's kernels whatever
+            # torch's current stream is (a blocking copy: it returns once the bytes are on the host)
+            with torch.cuda.stream(self._stream):
+                self._host_buf.copy_(self._out_buf)
         if copy:
             return {name: v.copy() for name, v in self._host_views.items()}
         return dict(self._host_views)
@@ -331,11 +346,9 @@ def _as_u8_device(t, n):
 _hip = None
 
 
-def _copy_device(dst, src, nbytes):
-    """hipMemcpy device->device through the HIP runtime (used once at construction)."""
+def _hip_lib():
     global _hip
     if _hip is None:
-        import ctypes.util
         for name in ("libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"):
             try:
                 _hip = C.CDLL(name)
@@ -346,6 +359,24 @@ def _copy_device(dst, src, nbytes):
             raise RuntimeError("libamdhip64 not found")
         _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         _hip.hipMemcpy.restype = C.c_int
-    rc = _hip.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, 3)  # hipMemcpyDeviceToDevice
+        _hip.hipHostGetDevicePointer.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_uint]
+        _hip.hipHostGetDevicePointer.restype = C.c_int
+    return _hip
+
+
+def _host_device_pointer(host_ptr):
+    """The device-side address of pinned host memory (hipHostGetDevicePointer); an error, never a
+    guess, if the runtime has no mapping for it."""
+    d = C.c_void_p()
+    rc = _hip_lib().hipHostGetDevicePointer(C.byref(d), C.c_void_p(host_ptr), 0)
+    if rc != 0 or not d.value:
+        raise RuntimeError("pinned output buffer has no device mapping (hipHostGetDevicePointer: %d)" % rc)
+    return d.value
+
+
+def _copy_device(dst, src, nbytes):
+    """hipMemcpy from device memory to a bound output buffer (device, or pinned host with
+    host_outputs) through the HIP runtime (used once at construction)."""
+    rc = _hip_lib().hipMemcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, 4)  # hipMemcpyDefault (dst may be pinned host)
     if rc != 0:
         raise RuntimeError("hipMemcpy failed: %d" % rc)

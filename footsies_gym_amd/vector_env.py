@@ -100,13 +100,15 @@ class FootsiesVectorEnv(_VectorEnvBase):
 
     def __init__(self, num_envs, device=0, opponent=None, dense_reward=True, frame_delay=0,
                  autoreset_mode="same_step", float_mode="strict", seed=0, vs_player=False, by_example=False,
-                 output="numpy"):
+                 output="numpy", _host_outputs=False):
         if vs_player:
             raise ValueError("vs_player needs a human at the game window; not available in the simulator")
         if not 0 <= int(frame_delay) <= _abi.FS_MAX_FRAME_DELAY:
             raise ValueError("frame_delay must be in [0, %d]" % _abi.FS_MAX_FRAME_DELAY)
         if output not in ("numpy", "torch"):
             raise ValueError("output must be 'numpy' or 'torch'")
+        if _host_outputs and output != "numpy":
+            raise ValueError("host-memory outputs serve the numpy output only")
         self.num_envs = int(num_envs)
         self.output = output
         self.autoreset_mode = autoreset_mode
@@ -118,7 +120,8 @@ class FootsiesVectorEnv(_VectorEnvBase):
         self.by_example = bool(by_example)
         self.sim = FootsiesSim(self.num_envs, device=device, p2_mode=p2, dense_reward=dense_reward,
                                float_mode=float_mode, autoreset_mode=autoreset_mode, seed=seed,
-                               frame_delay=frame_delay, p1_mode="bot" if by_example else "external")
+                               frame_delay=frame_delay, p1_mode="bot" if by_example else "external",
+                               host_outputs=_host_outputs)
         self._p2_bot = np.zeros(self.num_envs, dtype=bool)  # arenas switched to the bot (set_opponent)
         self._all_bot = False  # == self._p2_bot.all(), kept beside it (step reads it every call)
         self.single_observation_space = sp.single_observation_space()
@@ -307,9 +310,11 @@ class FootsiesEnv(_EnvBase):
         self._opp = opponent
         # next_step auto-reset keeps FE's handshake: a terminal step() returns the terminal
         # obs and the agent's reset() then finds the game already at state(-1) (no RESET)
+        # (one arena: the kernels write its outputs straight into pinned host memory, FootsiesSim
+        # host_outputs, so a step costs one launch and one stream synchronize, no copies)
         self.venv = FootsiesVectorEnv(1, device=device, opponent=self._wrap(opponent), dense_reward=dense_reward,
                                       frame_delay=frame_delay, seed=seed, autoreset_mode="next_step",
-                                      by_example=by_example)
+                                      by_example=by_example, _host_outputs=True)
         self.observation_space = self.venv.single_observation_space
         self.action_space = self.venv.single_action_space
         self.reward_range = (-1, 1)

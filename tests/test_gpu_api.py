@@ -586,3 +586,31 @@ def test_single_env_step_equals_one_arena_vector_env(opponent):
         assert seen
     single.close()
     venv.close()
+
+
+@pytest.mark.parametrize("n,p2", [(1, "bot"), (5, "external")])
+def test_host_outputs_equal_device_outputs(n, p2):
+    """FootsiesSim(host_outputs=True) -- the kernels write the outputs into pinned host memory --
+    gives the outputs of a device-output handle, step for step, over terminals and resets."""
+    from footsies_gym_amd.simulator import FootsiesSim
+    a, b = FootsiesSim(n, p2_mode=p2, seed=4), FootsiesSim(n, p2_mode=p2, seed=4, host_outputs=True)
+    assert not b.outputs()["guard"].is_cuda
+    compare_outputs(a.outputs_numpy(), b.outputs_numpy(), step=-1)
+    rng = np.random.default_rng(9)
+    terminals = 0
+    for t in range(3000):
+        a1, a2 = rng.integers(0, 8, n).astype(np.uint8), rng.integers(0, 8, n).astype(np.uint8)
+        q2 = a2 if p2 == "external" else None
+        a.step(a1, q2)
+        b.step(a1, q2)
+        oa, ob = a.outputs_numpy(), b.outputs_numpy()
+        compare_outputs(oa, ob, step=t)
+        terminals += int(oa["terminated"].sum())
+        if t % 700 == 0:
+            a.reset(hard=True)
+            b.reset(hard=True)
+            compare_outputs(a.outputs_numpy(), b.outputs_numpy(), step=t)
+    assert terminals > 0
+    compare_states(a.get_state(), b.get_state(), step=3000)
+    a.close()
+    b.close()
