@@ -62,8 +62,9 @@ class SimBackend:
 
     def __init__(self, p2_bot=True, dense_reward=True, device=0, seed=0):
         from .simulator import FootsiesSim
+        # (one arena: outputs written into pinned host memory, see FootsiesSim host_outputs)
         self.sim = FootsiesSim(1, p2_mode="bot" if p2_bot else "external", seed=seed, device=device,
-                               dense_reward=dense_reward, autoreset_mode="next_step")
+                               dense_reward=dense_reward, autoreset_mode="next_step", host_outputs=True)
 
     def env_state(self):
         return self.sim.env_state()[0]
@@ -71,7 +72,7 @@ class SimBackend:
     def step(self, p1, p2):
         self.sim.step(np.array([p1], np.uint8), np.array([0 if p2 is None else p2], np.uint8)
                       if self.sim.p2_mode == "external" else None)
-        return bool(self.sim.outputs_numpy()["terminated"][0])
+        return bool(self.sim.outputs_numpy(copy=False)["terminated"][0])
 
     def reset(self, hard):
         self.sim.reset(hard=hard)
