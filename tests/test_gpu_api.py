@@ -550,8 +550,8 @@ def test_single_env_after_close_raises_game_closed_error():
         env.reset()
 
 
-@pytest.mark.parametrize("opponent", [None, "callable"])
-def test_single_env_step_equals_one_arena_vector_env(opponent):
+@pytest.mark.parametrize("opponent,delay", [(None, 0), ("callable", 0), (None, 2)])
+def test_single_env_step_equals_one_arena_vector_env(opponent, delay):
     """FootsiesEnv.step (its direct host conversion) == FootsiesVectorEnv(1, next-step auto-reset)
     through the batch path, step for step over terminations, with the bot or a remote P2."""
     from footsies_gym_amd.simulator import encode_actions
@@ -561,12 +561,12 @@ def test_single_env_step_equals_one_arena_vector_env(opponent):
     def opp(obs, info):  # reads the agent's most recent single-arena dicts (FE:525-527)
         seen.append(obs["position"])
         return (False, obs["position"][0] < 0, True)
-    single = FootsiesEnv(seed=3, opponent=None if opponent is None else opp)
+    single = FootsiesEnv(seed=3, opponent=None if opponent is None else opp, frame_delay=delay)
 
     def batch_opp(obs, info):  # the same P2 policy over the batch env's own (obs, info)
         return np.array([encode_actions([opp(*FootsiesEnv._py(obs, info))])[0]], np.uint8)
     wrapped = None if opponent is None else batch_opp
-    venv = FootsiesVectorEnv(1, seed=3, autoreset_mode="next_step", opponent=wrapped)
+    venv = FootsiesVectorEnv(1, seed=3, autoreset_mode="next_step", opponent=wrapped, frame_delay=delay)
     rng = np.random.default_rng(5)
     o1, i1 = single.reset(seed=3)
     o2, i2 = FootsiesEnv._py(*venv.reset(seed=3))
