@@ -91,6 +91,8 @@ class FootsiesVectorEnv(_VectorEnvBase):
     ``by_example`` (FE:83-84, 118, 230-232): the in-game bot plays P1 as well and the agent only
     observes -- ``step`` ignores its actions (FE:522-523).
     ``output="torch"`` returns device tensors (zero-copy) instead of numpy.
+    (``_host_outputs``, internal: the kernels write the outputs into pinned host memory --
+    FootsiesSim ``host_outputs`` -- for the one-arena FootsiesEnv; numpy output only.)
     """
 
     metadata = {"render_modes": [], "render_fps": 60}
