@@ -438,7 +438,9 @@ template <int FM, int P2>
 __device__ __forceinline__ void step_body1(const StepParams& p) {
   constexpr int D = FS_ROW_DEPTH;
   constexpr int W = 12 * (D - 1);
-  static_assert(D >= 2 && W <= 63, "row pipeline depth");
+  // (the main loop below unrolls at most four ticks per iteration and the remainder handles at most
+  // three, so a deeper pipeline would skip ticks; vmcnt's 6-bit field bounds W as well)
+  static_assert(D >= 2 && D <= 4 && W <= 63, "row pipeline depth 2..4");
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = a < p.n_envs;
   const int ar = active ? a : 0;

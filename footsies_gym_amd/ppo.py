@@ -115,19 +115,13 @@ class PPOGrad:
 
     def __init__(self, actor, critic):
         torch = _torch()
-        nets = []
-        for net, out in ((actor, N_ACTIONS), (critic, 1)):
-            lin = [m for m in net if isinstance(m, torch.nn.Linear)]
-            acts = [m for m in net if not isinstance(m, torch.nn.Linear)]
-            shapes = [tuple(m.weight.shape) for m in lin]
-            if shapes != [(64, N_FEATURES), (64, 64), (out, 64)] or not all(isinstance(m, torch.nn.Tanh) for m in acts):
-                raise ValueError("the fused learner takes 8-64-64-%d tanh MLPs; got %s" % (out, shapes))
-            params = [t for m in lin for t in (m.weight, m.bias)]
-            if any(t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() for t in params):
-                raise ValueError("the fused learner needs contiguous fp32 device parameters")
-            nets.append(params)
+        self._modules = (actor, critic)
+        nets = self._collect()
         dev = nets[0][0].device
+        self.device = dev
+        self._nets = nets
         self.params = nets[0] + nets[1]
+        self._validate(self.params)
         self.grad = torch.zeros(_abi.FS_PPO_ACTOR_PARAMS + _abi.FS_PPO_CRITIC_PARAMS, dtype=torch.float32, device=dev)
         off = 0
         for p in self.params:
@@ -136,9 +130,32 @@ class PPOGrad:
         assert off == self.grad.numel()
         self.loss = torch.zeros(3, dtype=torch.float32, device=dev)
         self.workspace = torch.empty(lib().fs_ppo_workspace_bytes(), dtype=torch.uint8, device=dev)
-        self._nets = nets
         self._bind()
-        self.device = dev
+
+    def _collect(self):
+        """The parameters as the modules hold them now: [weight, bias] x 3 per network (a module
+        whose weight was replaced -- load_state_dict(assign=True), m.weight = nn.Parameter(...) --
+        yields the new tensor)."""
+        torch = _torch()
+        nets = []
+        for net, out in zip(self._modules, (N_ACTIONS, 1)):
+            lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+            acts = [m for m in net if not isinstance(m, torch.nn.Linear)]
+            shapes = [tuple(m.weight.shape) for m in lin]
+            if shapes != [(64, N_FEATURES), (64, 64), (out, 64)] or not all(isinstance(m, torch.nn.Tanh) for m in acts):
+                raise ValueError("the fused learner takes 8-64-64-%d tanh MLPs; got %s" % (out, shapes))
+            if any(m.bias is None for m in lin):
+                raise ValueError("the fused learner needs every Linear to have a bias")
+            nets.append([t for m in lin for t in (m.weight, m.bias)])
+        return nets
+
+    def _validate(self, params):
+        torch = _torch()
+        for t in params:
+            if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+                raise ValueError("the fused learner needs contiguous fp32 device parameters")
+            if t.device != self.device:
+                raise ValueError("parameter on %s, but the fused learner was built on %s" % (t.device, self.device))
 
     def _bind(self):
         """The kernels' view of the parameters: raw device pointers of every weight and bias."""
@@ -146,19 +163,25 @@ class PPOGrad:
         self._ptrs = [p.data_ptr() for p in self.params]
 
     def _check_bindings(self):
-        """Before a launch: every parameter's .grad must still be its view of the flat buffer the
-        kernel writes (an optimizer's zero_grad(set_to_none=True) drops it; it is re-attached --
-        the kernel overwrites the whole buffer), and every parameter must still live where the
-        kernel reads it (param.data = ..., .to(): the pointers are re-read)."""
+        """Before a launch: the parameters are re-collected from the modules (a module whose weight
+        or bias was replaced by a new tensor is seen), each must still be a contiguous fp32 tensor
+        on this learner's device, every .grad must still be its view of the flat buffer the kernel
+        writes (an optimizer's zero_grad(set_to_none=True) drops it; it is re-attached -- the
+        kernel overwrites the whole buffer), and the kernel's pointers are re-read when any
+        parameter moved (param.data = ..., a new Parameter)."""
+        nets = self._collect()
+        params = nets[0] + nets[1]
+        moved = [p.data_ptr() for p in params] != self._ptrs or any(a is not b for a, b in zip(params, self.params))
+        if moved:
+            self._validate(params)
+            self._nets, self.params = nets, params
         off = 0
         base = self.grad.data_ptr()
         for p in self.params:
             if p.grad is None or p.grad.data_ptr() != base + 4 * off or p.grad.shape != p.shape:
                 p.grad = self.grad[off:off + p.numel()].view_as(p)
             off += p.numel()
-        if [p.data_ptr() for p in self.params] != self._ptrs:
-            if any(t.dtype != _torch().float32 or not t.is_cuda or not t.is_contiguous() for t in self.params):
-                raise ValueError("the fused learner needs contiguous fp32 device parameters")
+        if moved:
             self._bind()
 
     def evaluate(self, x, actions=None, n_logp=0):

@@ -72,7 +72,7 @@ class SimBackend:
     def step(self, p1, p2):
         self.sim.step(np.array([p1], np.uint8), np.array([0 if p2 is None else p2], np.uint8)
                       if self.sim.p2_mode == "external" else None)
-        return bool(self.sim.outputs_numpy(copy=False)["terminated"][0])
+        return bool(self.sim.outputs_numpy(copy=False, _synced=True)["terminated"][0])  # (step waited)
 
     def reset(self, hard):
         self.sim.reset(hard=hard)

@@ -100,7 +100,9 @@ class FootsiesSim:
         # host_outputs: the bound buffers are pinned host memory, which the kernels write across
         # the bus; a step's outputs are then on the host once the stream is done, with no copy
         # (the single-arena drop-in, where the copy's own latency was a third of a step).
-        # outputs() then returns host tensors.
+        # outputs() then returns host tensors; every call that returns them (step, reset, step_n
+        # without a trajectory, outputs) first waits for the handle's stream, so they never hold
+        # an earlier tick's values while the kernels are still writing (_host_ready).
         self.host_outputs = bool(host_outputs)
         if self.host_outputs:
             self._out_buf = torch.zeros(total, dtype=torch.uint8, pin_memory=True)
@@ -147,7 +149,7 @@ class FootsiesSim:
         flags = _abi.FS_RESET_SEED_ONLY if seed_only else (_abi.FS_RESET_HARD if hard else _abi.FS_RESET_IF_NEEDED)
         check(lib().fs_reset(self._h, None if s is None else s.ctypes.data, None if m is None else m.ctypes.data,
                              flags), self._h)
-        return self._out
+        return self._ready_out()
 
     def set_p2_mode(self, mode, mask=None):
         """P2 of the masked arenas (all by default) becomes the in-game bot (mode "bot") or the
@@ -172,7 +174,7 @@ class FootsiesSim:
             rc = lib().fs_step(self._h, p1.data_ptr(), p2.data_ptr() if ext else None, _abi.FS_ACT_DEVICE)
             if rc:
                 check(rc, self._h)
-            return self._out
+            return self._ready_out()
         if ext and p2 is None:
             raise ValueError("p2 actions are required when p2_mode='external'")
         if p1 is None:
@@ -203,7 +205,7 @@ class FootsiesSim:
             else:
                 m = np.ascontiguousarray(np.asarray(active).reshape(self.num_envs), dtype=np.uint8)
                 check(lib().fs_step_masked(self._h, a1.ctypes.data, q2, m.ctypes.data, _abi.FS_ACT_HOST), self._h)
-        return self._out
+        return self._ready_out()
 
     def step_n(self, n, p1=None, p2=None, action_seed=0, trajectory=None):
         """n ticks in one kernel launch.  p1/p2: device uint8 [n][N] or None (on-device hashed
@@ -214,7 +216,7 @@ class FootsiesSim:
         check(lib().fs_step_n(self._h, int(n), None if p1 is None else C.c_void_p(p1.data_ptr()),
                               None if p2 is None else C.c_void_p(p2.data_ptr()), int(action_seed) & (2**64 - 1),
                               None if t is None else C.byref(t)), self._h)
-        return trajectory if trajectory is not None else self._out
+        return trajectory if trajectory is not None else self._ready_out()
 
     def hash_actions(self, n_steps, seed=0x5EED, t0=0, p2=True):
         """Device uint8 [n_steps][N] action arrays from the synthetic splitmix64 stream."""
@@ -234,6 +236,14 @@ class FootsiesSim:
         return out
 
     def outputs(self):
+        return self._ready_out()
+
+    def _ready_out(self):
+        """The bound outputs, safe to read: with host_outputs the kernels write them into pinned
+        host memory asynchronously, so the handle's stream is waited for first (device tensors are
+        ordered by the stream and need no wait)."""
+        if self.host_outputs:
+            check(lib().fs_sync(self._h), self._h)
         return self._out
 
     def pack_outputs(self, dst=None):
@@ -245,9 +255,11 @@ class FootsiesSim:
         check(lib().fs_pack_outputs(self._h, C.c_void_p(dst.data_ptr())), self._h)
         return dst
 
-    def outputs_numpy(self, copy=True):
+    def outputs_numpy(self, copy=True, _synced=False):
         """The current outputs on the host, fetched with one device-to-host copy into a pinned
-        buffer.  copy=False returns views of that buffer, overwritten by the next call."""
+        buffer.  copy=False returns views of that buffer, overwritten by the next call.
+        (_synced, internal: with host_outputs, the caller has just waited for the stream --
+        step / reset returned -- and nothing was issued since.)"""
         torch = _torch()
         if self._host_buf is None:
             self._host_buf = (self._out_buf if self.host_outputs else
@@ -257,7 +269,8 @@ class FootsiesSim:
             self._host_views = {name: host[off:off + nbytes].view(dt).reshape(shape)
                                 for name, dt, shape, off, nbytes in self._out_layout}
         if self.host_outputs:  # the kernels wrote them there: wait for the handle's stream
-            check(lib().fs_sync(self._h), self._h)
+            if not _synced:
+                check(lib().fs_sync(self._h), self._h)
         else:
             # on the handle's own stream, so the copy is ordered after the library's kernels whatever
             # torch's current stream is (a blocking copy: it returns once the bytes are on the host)

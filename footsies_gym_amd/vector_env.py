@@ -149,7 +149,7 @@ class FootsiesVectorEnv(_VectorEnvBase):
         if self.output == "torch":
             self._last = (out, None)
             return {k: out[k] for k in ("guard", "move", "move_frame", "position")}, out
-        obs, info = obs_info_from_outputs(self.sim.outputs_numpy(copy=False))
+        obs, info = obs_info_from_outputs(self.sim.outputs_numpy(copy=False, _synced=True))  # (reset waited)
         self._last = (obs, info)
         return obs, info
 
@@ -201,7 +201,8 @@ class FootsiesVectorEnv(_VectorEnvBase):
             obs = {k: out[k] for k in ("guard", "move", "move_frame", "position")}
             self._last = (obs, out)
             return obs, out["reward"], out["terminated"], out["truncated"], out
-        obs, rew, term, trunc, info = step_result_from_outputs(self.sim.outputs_numpy(copy=False), self.autoreset_mode)
+        obs, rew, term, trunc, info = step_result_from_outputs(self.sim.outputs_numpy(copy=False, _synced=True),
+                                                               self.autoreset_mode)  # (step waited)
         self._last = (obs, info)
         return obs, rew, term, trunc, info
 
@@ -377,7 +378,7 @@ class FootsiesEnv(_EnvBase):
         v._check_open()
         p2 = v._p2_actions()
         v.sim.step(None if v.by_example else np.asarray([action]).reshape(1, 3), p2)
-        h = v.sim.outputs_numpy(copy=False)
+        h = v.sim.outputs_numpy(copy=False, _synced=True)  # (step waited for the host outputs)
         o, i = self._py_host(h)
         v._last = (o, i)  # (the wrapped opponent reads this env's most recent dicts, not these)
         self._most_recent_observation, self._most_recent_info = dict(o), dict(i)

@@ -5,7 +5,7 @@ import pytest
 
 from footsies_gym_amd import _abi
 from tests import golden_utils as gu
-from tests import kat_combat
+from tests import kat_combat, kat_core
 from tests import kat_scenarios as kat
 from tests import wire_client, wire_replay
 from tests import wrapper_replay as wr
@@ -25,6 +25,12 @@ def test_kat_gpu(name):
 @pytest.mark.parametrize("name", sorted(kat_combat.ALL))
 def test_kat_combat_gpu(name):
     kat_combat.ALL[name](SimBackend(1))
+
+
+@pytest.mark.parametrize("name", sorted(kat_core.ALL))
+def test_kat_core_gpu(name):
+    """tests/kat_core.py (the sim-core paths round 3 pinned only by lockstep) through the HIP path."""
+    kat_core.ALL[name](SimBackend(1))
 
 
 @pytest.mark.parametrize("name", gu.CASES)
@@ -612,5 +618,34 @@ def test_host_outputs_equal_device_outputs(n, p2):
             compare_outputs(a.outputs_numpy(), b.outputs_numpy(), step=t)
     assert terminals > 0
     compare_states(a.get_state(), b.get_state(), step=3000)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("p2", ["bot", "external"])
+def test_host_outputs_read_straight_from_step(p2):
+    """With host_outputs the tensors sim.step / sim.reset / sim.outputs return are pinned host
+    memory the kernels write asynchronously; each of those calls waits for the handle's stream
+    first, so reading them at once gives this tick's values (advisor r03: they could hold the
+    previous tick's).  Read with no outputs_numpy call in between, against a device-output twin."""
+    from footsies_gym_amd.simulator import FootsiesSim
+    n = 7
+    a, b = FootsiesSim(n, p2_mode=p2, seed=11), FootsiesSim(n, p2_mode=p2, seed=11, host_outputs=True)
+    rng = np.random.default_rng(3)
+    terminals = 0
+    for t in range(600):
+        a1, a2 = rng.integers(0, 8, n).astype(np.uint8), rng.integers(0, 8, n).astype(np.uint8)
+        q2 = a2 if p2 == "external" else None
+        a.step(a1, q2)
+        out = b.step(a1, q2)  # read immediately: no sync by the caller
+        got = {k: v.numpy().copy() for k, v in out.items()}
+        compare_outputs(a.outputs_numpy(), got, step=t)
+        terminals += int(got["terminated"].sum())
+        if t % 250 == 249:
+            a.reset(hard=True)
+            got = {k: v.numpy().copy() for k, v in b.reset(hard=True).items()}
+            compare_outputs(a.outputs_numpy(), got, step=t)
+            compare_outputs(a.outputs_numpy(), {k: v.numpy().copy() for k, v in b.outputs().items()}, step=t)
+    assert terminals > 0
     a.close()
     b.close()

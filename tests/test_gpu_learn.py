@@ -208,3 +208,30 @@ def test_ppo_features_match_obs_features():
         assert torch.equal(out[t], obs_features({k: tr[k][t] for k in ("guard", "move", "move_frame", "position")}))
     with pytest.raises(ValueError):
         features_device(tr, out[:, :, :4])
+
+
+def test_ppo_grad_follows_replaced_parameters():
+    """PPOGrad re-collects the parameters from the modules before every launch (advisor r03): a
+    weight replaced by a new Parameter (m.weight = nn.Parameter(...), as load_state_dict(assign=
+    True) does) is the one the kernel reads and whose .grad it fills, so the gradient equals the
+    fresh learner's on the same weights; a parameter moved off the learner's device is refused."""
+    import torch
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=3)
+    rows = _rows(actor, 4096, seed=3)
+    pg = PPOGrad(actor, critic)
+    pg(rows, 0.2, 0.5, 0.01)
+    lin = [m for m in actor if isinstance(m, torch.nn.Linear)]
+    lin[1].weight = torch.nn.Parameter(lin[1].weight.detach() * 0.5 + 0.01)
+    loss = pg(rows, 0.2, 0.5, 0.01).clone()
+    got = [p.grad.detach().clone() for p in pg.params]
+    assert pg.params[2] is lin[1].weight and lin[1].weight.grad is not None
+    fresh = PPOGrad(actor, critic)
+    ref_loss = fresh(rows, 0.2, 0.5, 0.01).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(loss, ref_loss)
+    for g, e in zip(got, [p.grad for p in fresh.params]):
+        assert torch.equal(g, e)
+    lin[0].bias = torch.nn.Parameter(lin[0].bias.detach().cpu())
+    with pytest.raises(ValueError):
+        pg(rows, 0.2, 0.5, 0.01)

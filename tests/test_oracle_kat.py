@@ -2,7 +2,7 @@
 import pytest
 
 from footsies_gym_amd import _abi
-from tests import kat_actors, kat_combat
+from tests import kat_actors, kat_combat, kat_core
 from tests import kat_scenarios as kat
 
 
@@ -20,6 +20,17 @@ def test_kat_actors_oracle(oracle_lib, name):
 @pytest.mark.parametrize("name", sorted(kat_combat.ALL))
 def test_kat_combat_oracle(oracle_lib, name):
     kat_combat.ALL[name](kat_combat.OracleKat(oracle_lib))
+
+
+@pytest.mark.parametrize("name", sorted(kat_core.ALL))
+def test_kat_core_oracle(oracle_lib, name):
+    """The sim-core paths pinned by hand-derived scenarios (tests/kat_core.py) on the oracle."""
+    kat_core.ALL[name](kat_combat.OracleKat(oracle_lib))
+
+
+def test_kat_core_covers_its_pin_table():
+    from tests import kat_core as K
+    assert set(K.ALL) == set(K.PINS)
 
 
 def test_kat_bot_plans_oracle(oracle_lib):
