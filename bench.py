@@ -35,11 +35,15 @@ MI355X_SIMDS = 256 * 4  # CUs x SIMDs per CU (MI355X_MICROARCH.md)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (8.0 TB/s spec)
 STATE_BYTES = 96        # per arena per launch: 48 B state read + 48 B written (fs_kernels.hip layout)
 STEP_IO_BYTES = 40      # per env-step: 2 B actions in + 38 B outputs out (include/footsies.h fs_outputs)
+XGMI_LINK_GBPS = 153.0  # per xGMI link and direction (task brief: 7 links x ~153 GB/s per MI355X)
+LEG_TICKS = 1000        # ticks per region (and per launch) of the fused side legs, whatever --steps is
+VENV_STEPS = 200        # timed FootsiesVectorEnv steps, after a warm-up into steady state
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: the launcher's WORLD_SIZE, else 1")
     # SURVEY 8(d)'s C3 protocol: 200 warm-up steps, then 5 timed runs of 2 000 steps (median)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
@@ -122,32 +126,54 @@ def cpu_baseline(envs, seconds, seed):
                               "sample": "%d arenas x %d steps, 1 thread, %.1f s" % (envs, steps1, dt1)}}
 
 
-def bot_mode_rate(torch, N, K, W, chunk, seed, device):
-    """Config C2's opponent at the C3 size: P1 random (HBM), P2 the in-kernel BattleAI, fused."""
-    import ctypes as C
+def fused_leg(torch, N, ticks, chunk, seed, device, rank, kind):
+    """A fused-mode leg on its own handle, set up untimed; returns (run(k0, n), kernel name, close).
+    kind "bot" = config C2's opponent at this size: P1 random (HBM), P2 the in-kernel BattleAI.
+    kind "mixed_p2" = the per-arena actors (kActors, BC:158-167 P2_BOT): a remote-P2 handle with P2
+    switched to the bot in every other arena (FE:458-480 set_opponent), both players' rows read.
+    kind "by_example" = the bot as P1 too (GameManager.cs:87, 185-189; FE:118), P2 the bot."""
     from footsies_gym_amd import _abi
     from footsies_gym_amd._lib import check, lib
     from footsies_gym_amd.simulator import FootsiesSim
-    sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
-    p1, _ = sim.hash_actions(W + K, seed=seed, p2=False)
+    import numpy as np
+    if kind == "bot":
+        sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0, arena_base=rank * N)
+    elif kind == "mixed_p2":
+        sim = FootsiesSim(N, device=device, p2_mode="external", seed=0, arena_base=rank * N)
+        sim.set_p2_mode("bot", (np.arange(N) % 2 == 0).astype(np.uint8))
+    elif kind == "by_example":
+        sim = FootsiesSim(N, device=device, p2_mode="bot", p1_mode="bot", seed=0, arena_base=rank * N)
+    else:
+        raise ValueError(kind)
+    ext = kind == "mixed_p2"
+    p1, p2 = sim.hash_actions(ticks, seed=seed, p2=ext)
     traj = sim.alloc_trajectory(chunk)
     td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+    h, L = sim.handle, lib()
+    b1 = p1.data_ptr()
+    b2 = p2.data_ptr() if ext else None
 
     def run(k0, n):
         k = k0
         while k < k0 + n:
             m = min(chunk, k0 + n - k)
-            check(lib().fs_step_n(sim.handle, m, C.c_void_p(p1.data_ptr() + k * N), None, 0, C.byref(td)), sim.handle)
+            q2 = C.c_void_p(b2 + k * N) if ext else None
+            rc = L.fs_step_n(h, m, C.c_void_p(b1 + k * N), q2, 0, C.byref(td))
+            if rc:
+                check(rc, h)
             k += m
-    run(0, W)
-    torch.cuda.synchronize(device)
-    t = time.perf_counter()
-    run(W, K)
-    torch.cuda.synchronize(device)
-    dt = time.perf_counter() - t
-    sim.close()
-    return {"value": N * K / dt, "ms_per_step": 1e3 * dt / K, "kernel": "fsk::k_step_n<0, 1>",
-            "config": "C2 opponent: P1 random actions, P2 = in-kernel BattleAI, %d arenas" % N}
+    kname = L.fs_step_kernel(h, chunk, 0).decode()
+
+    def close():
+        sim.close()
+    return run, kname, close
+
+
+LEG_CONFIG = {
+    "bot": "C2 opponent: P1 random actions, P2 = in-kernel BattleAI",
+    "mixed_p2": "per-arena actors: P2 remote in odd arenas, switched to the bot in even ones (set_opponent / P2_BOT)",
+    "by_example": "by_example: the BattleAI plays P1 and P2 (bot vs bot, the agent observes)",
+}
 
 
 def policy_loop_rate(torch, N, steps, device):
@@ -221,15 +247,18 @@ def ppo_rate(torch, N, device, horizon=128, iterations=3):
                       % (N, horizon)}
 
 
-def vector_env_rate(torch, N, steps, device):
+def vector_env_rate(torch, N, steps, device, warm=400):
     """The drop-in surface itself at the C3 size: FootsiesVectorEnv.step with numpy (N,) int
-    actions in and numpy obs / reward / info out (the D2H copy and the dict building of every
-    step included), P2 a callable opponent returning pre-drawn numpy actions; then the same
-    env with output="torch": device actions in, device tensors out (zero-copy)."""
+    actions in and numpy obs / reward / info out (the D2H copy, the conversions and gymnasium
+    0.29's per-arena final_observation / final_info dicts of every step included), P2 a callable
+    opponent returning pre-drawn numpy actions; then the same env with output="torch": device
+    actions in, device tensors out (zero-copy).  `warm` untimed steps first, so the timed steps
+    run at the steady terminal rate (right after a reset no episode can end for tens of steps),
+    and `steps` timed steps whatever the bench's --steps is; the terminal count of the timed
+    steps is reported."""
     import numpy as np
     from footsies_gym_amd.vector_env import FootsiesVectorEnv
     rng = np.random.default_rng(0)
-    warm = 5
     a1 = rng.integers(0, 8, (warm + steps, N)).astype(np.uint8)
     a2 = rng.integers(0, 8, (warm + steps, N)).astype(np.uint8)
     out = {}
@@ -247,16 +276,20 @@ def vector_env_rate(torch, N, steps, device):
             k[0] = j
             env.step(acts[j])
         torch.cuda.synchronize(device)
+        terms = []
         t = time.perf_counter()
         for j in range(warm, warm + steps):
             k[0] = j
-            env.step(acts[j])
+            terms.append(env.step(acts[j])[2])
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t
         env.close()
-        out[kind] = {"value": N * steps / dt, "ms_per_step": 1e3 * dt / steps, "steps": steps}
+        nterm = int(sum(int(x.sum()) for x in terms))
+        out[kind] = {"value": N * steps / dt, "ms_per_step": 1e3 * dt / steps, "steps": steps,
+                     "warmup_steps": warm, "terminals_per_step": nterm / steps}
     out["config"] = ("FootsiesVectorEnv(%d, opponent=callable).step: numpy actions -> numpy obs/info dicts "
-                     "(D2H + conversion every step), and output='torch' (device tensors in/out)" % N)
+                     "(D2H + conversion every step, final_observation dicts for the terminated arenas), and "
+                     "output='torch' (device tensors in/out); steady state after the warm-up" % N)
     return out
 
 
@@ -395,15 +428,17 @@ def dry_run(args, world, rank):
 
 def main():
     args = parse()
-    if args.gpus < 1:
+    if args.gpus is not None and args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # the driver's plain `python3 bench.py --gpus N`: start the N ranks (nothing has touched the GPU)
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus:
+    # under a launcher, --gpus may be left out (the launcher's world size is taken); given, it must agree
+    if args.gpus is not None and world != args.gpus:
         raise SystemExit("bench.py --gpus %d, but the launcher started %d rank(s) (WORLD_SIZE)" % (args.gpus, world))
+    args.gpus = world
     if args.dry_run:
         return dry_run(args, world, rank)
     import torch
@@ -616,12 +651,13 @@ def main():
         kt, kmed, bytes_per_launch = roofline_at(rt, rfn, rlo, rhi, max(5, args.kernel_samples // 10))
         ticks = rt
         st_kt, st_kmed, st_bytes = roofline_at(chunk, run_fused, W, W + R * K, max(5, args.kernel_samples // 5))
-        kname = "fsk::k_step_n<0, 0>"
+        kname = L.fs_step_kernel(h, rt, 0).decode()  # the kernel this launch shape runs (k_step_n1 from 2 x 64 x SIMDs arenas)
     else:
         kt, kmed, bytes_per_launch = roofline_at(1, run_step, W, W + R * K, args.kernel_samples)
         st_kt, st_kmed, st_bytes = kt, kmed, bytes_per_launch
         ticks = 1
-        kname = "fsk::k_step<0, 0>"
+        kname = L.fs_step_kernel(h, 1, 0).decode()
+    st_kname = L.fs_step_kernel(h, chunk if args.mode == "fused" else 1, 0).decode()
     achieved = bytes_per_launch / kt / 1e9
     tr = pmc_traffic(kname, N, ticks)
     issue = issue_profile(kname, N, ticks)
@@ -669,7 +705,8 @@ def main():
                                   "avg_launch_us": st_kt * 1e6, "median_launch_us": st_kmed * 1e6,
                                   "algorithmic_bytes_per_launch": st_bytes,
                                   "frac": st_bytes / st_kt / 1e9 / HBM_PEAK_GBPS,
-                                  "traffic": (pmc_traffic(kname, N, chunk if args.mode == "fused" else 1) or
+                                  "kernel": st_kname,
+                                  "traffic": (pmc_traffic(st_kname, N, chunk if args.mode == "fused" else 1) or
                                               (None,))[0]},
         other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
         "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
@@ -685,8 +722,47 @@ def main():
                                   "note": "fs_step + fs_pack_outputs + the records of every rank gathered to rank 0 "
                                           "only (grouped send / recv over RCCL, parallel.gather_records_to)"},
     }
+    # the fused legs beside the headline, on every rank (barrier + max over ranks, like the
+    # headline), at a fixed shape whatever --steps is: R regions of LEG_TICKS ticks in
+    # LEG_TICKS-tick launches, the median reported
+    if not args.no_extras:
+        for key, kind in (("p2_bot_mode", "bot"), ("actors_mode.mixed_p2", "mixed_p2"),
+                          ("actors_mode.by_example", "by_example")):
+            try:
+                run_leg, leg_kernel, close_leg = fused_leg(torch, N, LEG_TICKS * (R + 1), LEG_TICKS, args.seed, local,
+                                                           rank, kind)
+                lw = leg_median(run_leg, LEG_TICKS, LEG_TICKS)
+                close_leg()
+                v = {"value": world * N * LEG_TICKS / lw, "ms_per_step": 1e3 * lw / LEG_TICKS,
+                     "ticks_per_launch": LEG_TICKS, "kernel": leg_kernel, "config": LEG_CONFIG[kind] +
+                     ", %d arenas per GPU" % N}
+            except Exception as e:  # noqa: BLE001 - the headline line must still print
+                v = {"error": "%s: %s" % (type(e).__name__, e)}
+            if "." in key:
+                a, b = key.split(".")
+                out.setdefault(a, {})[b] = v
+            else:
+                out[key] = v
+    # the exchange alone: the same all_gather of the 40-B records with no simulation between
+    # them, its received bytes per rank against the xGMI links that carry them (one link per
+    # peer on a fully connected node; 7 links x ~153 GB/s per MI355X, the task brief -- the
+    # figure is not in MI355X_MICROARCH.md)
+    if grouped and args.dist_backend == "nccl" and world > 1:
+        def run_gather(k0, n):
+            for _ in range(n):
+                dist.all_gather_into_tensor(gbuf, rec)
+        gowall = leg_median(run_gather, 0, kg)
+        recv = (world - 1) * N * _abi.FS_RECORD_BYTES
+        out["step_gather_mode"]["xgmi"] = {
+            "bytes_received_per_rank_per_step": recv,
+            "gather_only_us_per_step": 1e6 * gowall / kg,
+            "link_GBps_per_rank": recv / (gowall / kg) / 1e9,
+            "in_step_GBps_per_rank": recv / (gwall / kg) / 1e9,
+            "peak_GBps_per_rank": (world - 1) * XGMI_LINK_GBPS,
+            "frac": recv / (gowall / kg) / 1e9 / ((world - 1) * XGMI_LINK_GBPS),
+            "note": "all_gather_into_tensor of every rank's [N, 40] records, alone (gather_only) and inside the "
+                    "fs_step + pack + gather step (in_step); peak = one ~153 GB/s xGMI link per peer"}
     if world == 1 and not args.no_extras:
-        out["p2_bot_mode"] = bot_mode_rate(torch, N, K, W, chunk, args.seed, local)
         try:
             out["policy_loop"] = policy_loop_rate(torch, N, min(K, 1000), local)
         except Exception as e:  # reported, never fatal to the headline measurement
@@ -700,20 +776,23 @@ def main():
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             out["ppo_end_to_end"] = {"error": "%s: %s" % (type(e).__name__, e)}
         try:
-            out["vector_env"] = vector_env_rate(torch, N, min(K, 200), local)
+            out["vector_env"] = vector_env_rate(torch, N, VENV_STEPS, local)
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             out["vector_env"] = {"error": "%s: %s" % (type(e).__name__, e)}
         try:
             out["single_env"] = single_env_rate(torch, 500, local)
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             out["single_env"] = {"error": "%s: %s" % (type(e).__name__, e)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    sim.close()
+    if grouped:
+        barrier()
+        dist.destroy_process_group()
+    # the CPU baseline last, on rank 0 alone: at N > 1 the other ranks have left, so the oracle
+    # has the host's cores to itself
+    if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.seed)
     if rank == 0:
         print(json.dumps(out))
-    sim.close()
-    if grouped:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

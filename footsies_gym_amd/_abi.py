@@ -37,6 +37,8 @@ FS_RESET_IF_NEEDED = 1
 FS_RESET_SEED_ONLY = 2
 FS_MAX_FRAME_DELAY = 4096
 FS_RECORD_BYTES = 40
+FS_KERNEL_HASHED = 1
+FS_KERNEL_POLICY = 2
 FS_PPO_ACTOR_PARAMS = 5256
 FS_PPO_CRITIC_PARAMS = 4801
 
@@ -168,6 +170,7 @@ LIB_FUNCTIONS = {
     "fs_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "fs_num_envs": (C.c_int, [C.c_void_p]),
     "fs_steps_taken": (C.c_uint64, [C.c_void_p]),
+    "fs_step_kernel": (C.c_char_p, [C.c_void_p, C.c_int, C.c_int]),
     "fs_destroy": (None, [C.c_void_p]),
     "fs_last_error": (C.c_char_p, [C.c_void_p]),
 }

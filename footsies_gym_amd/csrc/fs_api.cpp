@@ -737,6 +737,12 @@ FS_API int fs_set_stream(fs_handle h, void* stream) {
   return FS_OK;
 }
 
+FS_API const char* fs_step_kernel(fs_handle h, int n_steps, int flags) {
+  if (!h || n_steps <= 0 || (flags & ~(FS_KERNEL_HASHED | FS_KERNEL_POLICY))) return nullptr;
+  return fsk::step_kernel_name((flags & FS_KERNEL_POLICY) != 0, (flags & FS_KERNEL_HASHED) != 0, n_steps, h->n,
+                               h->cfg.float_mode, variant(h));
+}
+
 FS_API int fs_num_envs(fs_handle h) { return h ? h->n : 0; }
 FS_API uint64_t fs_steps_taken(fs_handle h) { return h ? h->steps : 0; }
 

@@ -69,7 +69,7 @@ __device__ __forceinline__ uint32_t bot_next_input1(Bot1& b, float dist, uint32_
   uint4 s2 = s1;
   const uint32_t x2 = rng_next(s2);
   const uint4 s0 = b.rng;
-  b.rng = (dm & da) ? s2 : (dm | da) ? s1 : s0;
+  b.rng = sel4(dm & da, s2, sel4(dm | da, s1, s0));
   const uint32_t newm = (pre.mw.map >> (4 * draw_mod(x1, pre.mw))) & 15u;
   const uint32_t drawn_a = (pre.aw.map >> (4 * draw_mod(dm ? x2 : x1, pre.aw))) & 15u;
   const uint32_t newa = forced ? (uint32_t)AP_TWO_HIT : drawn_a;

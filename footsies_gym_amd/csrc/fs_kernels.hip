@@ -30,6 +30,8 @@
 // AI = Assets/Script/BattleAI.cs, FE = footsies-gym/footsies_gym/envs/footsies.py.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "fs_internal.h"
 #include "fs_tables.h"
 #include "fs_policy.h"
@@ -523,6 +525,18 @@ __device__ __forceinline__ uint32_t rng_next(uint4& s) {  // UnityEngine.Random 
   s.w = s.w ^ (s.w >> 19) ^ t ^ (t >> 8);
   return s.w;
 }
+// A select between two uint4 values, one component at a time.  HIP's uint4 is a struct: a `c ? a :
+// b` on it is lowered through a private-memory copy and a dynamically addressed load (48-64 B of
+// scratch per lane in the per-arena-actor kernels before this helper); four 32-bit selects stay in
+// registers.
+__device__ __forceinline__ uint4 sel4(bool c, const uint4& a, const uint4& b) {
+  uint4 r;
+  r.x = c ? a.x : b.x;
+  r.y = c ? a.y : b.y;
+  r.z = c ? a.z : b.z;
+  r.w = c ? a.w : b.w;
+  return r;
+}
 __device__ __forceinline__ uint4 rng_init(int32_t seed) {  // Random.InitState
   uint4 s;
   s.x = (uint32_t)seed;
@@ -736,7 +750,7 @@ __device__ __forceinline__ uint32_t bot_next_input(Bot& b, uint32_t q, float dis
   uint4 s2 = s1;
   const uint32_t x2 = rng_next(s2);
   const uint4 s0 = b.rng;
-  b.rng = (dm & da) ? s2 : (dm | da) ? s1 : s0;
+  b.rng = sel4(dm & da, s2, sel4(dm | da, s1, s0));
   const BotDraw w = pre.w;
   const uint32_t drawn = (w.map >> (4 * draw_mod((!q & dm) ? x2 : x1, w))) & 15u;
   const uint32_t newp = (!q & forced) ? (uint32_t)AP_TWO_HIT : drawn;
@@ -1122,12 +1136,12 @@ __device__ __forceinline__ void actors_request(Lane& L, const Actors& ac, float 
   if (ac.p1_bot) {
     if (L.k == 0) L.bin = bot_full_next<G>(L.fb, r, 0, dist, p2_act);
     const uint4 o = xpair4(r);
-    r = L.k == 1 ? o : r;
+    r = sel4(L.k == 1, o, r);
   }
   if (L.p2bot) {
     if (L.k == 1) L.bin = bot_full_next<G>(L.fb, r, 1, dist, p1_act);
     const uint4 o = xpair4(r);
-    r = L.k == 0 ? o : r;
+    r = sel4(L.k == 0, o, r);
   }
   L.rng = r;
 }
@@ -1894,6 +1908,15 @@ static hipError_t launch_step_fm(const StepParams& p, int variant, hipStream_t s
 hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStream_t s) {
   return float_mode == FS_FLOAT_DOUBLE ? launch_step_fm<FS_FLOAT_DOUBLE>(p, variant, s)
                                        : launch_step_fm<FS_FLOAT_STRICT32>(p, variant, s);
+}
+
+// The kernel launch_step_p2 runs for a launch of this shape, as rocprofv3 names it (fs_step_kernel).
+const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant) {
+  static thread_local char buf[64];
+  const char* k = policy ? "k_step_n_policy" : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step"
+                : (variant != kActors && fused_one_lane(n_envs)) ? "k_step_n1" : "k_step_n";
+  snprintf(buf, sizeof buf, "fsk::%s<%d, %d>", k, float_mode == FS_FLOAT_DOUBLE ? 1 : 0, variant);
+  return buf;
 }
 
 hipError_t launch_reset(const ResetParams& p, int float_mode, hipStream_t s) {

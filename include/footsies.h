@@ -371,6 +371,15 @@ void* fs_stream(fs_handle h);
 int fs_set_stream(fs_handle h, void* stream);
 int fs_num_envs(fs_handle h);
 uint64_t fs_steps_taken(fs_handle h);
+/* The kernel a step call on h would launch, as rocprofv3 names it ("fsk::k_step_n<0, 0>"):
+ * n_steps = 1 is fs_step / fs_step_masked, n_steps > 1 fs_step_n with action rows (its launches
+ * pick the one-lane kernel from 2 x 64 x SIMD-count arenas on, FOOTSIES_FUSED_LANES forces
+ * either); flags FS_KERNEL_HASHED = fs_step_n without action rows, FS_KERNEL_POLICY =
+ * fs_step_n_policy.  For naming profiles and roofline lines; NULL for a bad handle or flags.
+ * The string stays valid until the calling thread's next call. */
+#define FS_KERNEL_HASHED 1
+#define FS_KERNEL_POLICY 2
+const char* fs_step_kernel(fs_handle h, int n_steps, int flags);
 void fs_destroy(fs_handle h);
 /* Last error message of h (or of the last failed fs_create when h is NULL). */
 const char* fs_last_error(fs_handle h);

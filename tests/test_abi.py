@@ -98,3 +98,11 @@ def test_simulator_requires_gpu():
     from footsies_gym_amd.simulator import FootsiesSim
     with pytest.raises(RuntimeError):
         FootsiesSim(8)
+
+
+def test_step_kernel_name_needs_a_handle(lib):
+    """fs_step_kernel (the kernel a step call launches, for profiles and the roofline line) answers
+    NULL without a handle; the names themselves are checked on the GPU (test_gpu_api.py)."""
+    f = lib.fs_step_kernel
+    f.restype, f.argtypes = _abi.LIB_FUNCTIONS["fs_step_kernel"]
+    assert f(None, 1, 0) is None

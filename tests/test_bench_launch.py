@@ -81,3 +81,34 @@ def test_launch_command(monkeypatch):
     assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
     assert cmd[-3:] == ["--gpus", "8", "--steps", "20"][-3:] and os.path.samefile(cmd[-5], BENCH)
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+def test_eight_ranks_dry_run():
+    """The driver's largest scaling point (N = 8) rehearsed on CPU: 8 gloo ranks, barriers, max over
+    ranks, one line from rank 0 whose value is the whole-job rate."""
+    p = run_bench(["--gpus", "8", "--dry-run", "--dist-backend", "gloo", "--steps", "10", "--regions", "3",
+                   "--envs", "500"], timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json_line(p.stdout)
+    assert out["n_gpus"] == 8 and out["ranks"]["world_size"] == 8 and len(out["ranks"]["rank_walls_ms"]) == 8
+    assert out["config"]["global_envs"] == 8 * 500
+    wall_s = out["ms_per_step"] * out["steps"] / 1e3
+    assert out["value"] == pytest.approx(8 * 500 * out["steps"] / wall_s, rel=1e-9)
+
+
+def test_outside_launcher_without_gpus_flag():
+    """`torchrun --nproc-per-node=2 bench.py` with no --gpus (advisor r03): the ranks take the
+    launcher's world size instead of refusing it."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", "--master-port=%d" % port, BENCH, "--dry-run", "--dist-backend",
+                        "gloo", "--steps", "5", "--regions", "2", "--envs", "100"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json_line(p.stdout)
+    assert out["n_gpus"] == 2 and out["ranks"]["world_size"] == 2

@@ -484,6 +484,28 @@ def test_bench_json_contract(extra):
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] >= 1
 
 
+def test_bench_extras_legs():
+    """The side legs of the bench line at a small size: the bot opponent (C2), the per-arena actors
+    (mixed P2 and by_example, the kActors kernels) each name the kernel that ran, and the
+    VectorEnv leg times steady steps whatever --steps is."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--envs", "2048", "--steps", "20", "--warmup", "5",
+           "--chunk", "20", "--roofline-ticks", "20", "--no-cpu-baseline", "--kernel-samples", "5"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, check=True).stdout
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["p2_bot_mode"]["kernel"] == "fsk::k_step_n<0, 1>" and d["p2_bot_mode"]["value"] > 0
+    for leg in ("mixed_p2", "by_example"):
+        assert d["actors_mode"][leg]["kernel"] == "fsk::k_step_n<0, 3>", d["actors_mode"]
+        assert d["actors_mode"][leg]["value"] > 0
+    assert d["roofline"]["kernel"] == "fsk::k_step_n<0, 0>"
+    v = d["vector_env"]["numpy"]
+    assert v["steps"] >= 200 and v["warmup_steps"] >= 200 and v["terminals_per_step"] > 0
+
+
 def test_native_consumer_under_host_sanitizers():
     """tests/native/abi_lockstep: a C++ program on include/footsies.h, built with host-side
     ASan + UBSan over a sanitizer build of the library's host code, steps the GPU in lockstep
@@ -649,3 +671,30 @@ def test_host_outputs_read_straight_from_step(p2):
     assert terminals > 0
     a.close()
     b.close()
+
+
+def test_step_kernel_names_the_launched_kernel():
+    """fs_step_kernel names the kernel launch_step picks (advisor r03: bench's roofline / PMC lookups
+    hard-coded k_step_n<0, 0>, which is not what runs from 131 072 arenas on)."""
+    import ctypes as C
+    import os
+    from footsies_gym_amd._lib import lib
+    from footsies_gym_amd.simulator import FootsiesSim
+    L = lib()
+    a = FootsiesSim(64, p2_mode="external")
+    name = lambda s, n, fl=0: L.fs_step_kernel(s.handle, n, fl).decode()  # noqa: E731
+    assert name(a, 1) == "fsk::k_step<0, 0>"
+    forced = os.environ.get("FOOTSIES_FUSED_LANES", "")
+    assert name(a, 1000) == ("fsk::k_step_n1<0, 0>" if forced == "1" else "fsk::k_step_n<0, 0>")
+    assert name(a, 1000, 1) == "fsk::k_step_n_hashed<0, 0>" and name(a, 20, 2) == "fsk::k_step_n_policy<0, 0>"
+    a.set_p2_mode("bot", np.arange(64) % 2 == 0)
+    assert name(a, 1000) == "fsk::k_step_n<0, 3>"  # per-arena actors
+    assert L.fs_step_kernel(a.handle, 0, 0) is None and L.fs_step_kernel(a.handle, 1, 8) is None
+    a.close()
+    b = FootsiesSim(64, p2_mode="bot", float_mode="double")
+    assert name(b, 1) == "fsk::k_step<1, 1>"
+    b.close()
+    big = FootsiesSim(131072, p2_mode="external")
+    if not forced:
+        assert name(big, 1000) == "fsk::k_step_n1<0, 0>"  # two one-lane waves per SIMD on MI355X
+    big.close()

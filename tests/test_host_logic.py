@@ -2,6 +2,7 @@
 info decoding (state.py:26-36), spaces (footsies.py:157-171), and the output -> (obs, info,
 reward, ...) conversion including gymnasium 0.29 same-step final_observation."""
 import json
+import os
 
 import numpy as np
 import pytest
@@ -9,6 +10,8 @@ import pytest
 from footsies_gym_amd import _abi, spaces
 from footsies_gym_amd.simulator import decode_actions, encode_actions
 from footsies_gym_amd.vector_env import obs_info_from_outputs, step_result_from_outputs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_encode_decode_roundtrip():
@@ -259,3 +262,17 @@ def test_single_env_host_conversion_equals_batch_path():
         (o1, i1), (o2, i2) = FootsiesEnv._py(obs, info), FootsiesEnv._py_host(h)
         assert o1 == o2 and i1 == i2 and list(i1) == list(i2)
         assert types(o1) == types(o2) and types(i1) == types(i2)
+
+
+def test_retain_host_heap_is_opt_out_and_idempotent():
+    """vector_env.retain_host_heap (mallopt: keep freed blocks on glibc's heap so a numpy step's
+    arrays do not re-fault their pages) applies once per process and honours FOOTSIES_NO_MALLOPT."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from footsies_gym_amd import vector_env as v; "
+            "print(v.retain_host_heap(), v.retain_host_heap())" % ROOT)
+    on = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout.split()
+    assert on == ["True", "True"]
+    env = dict(os.environ, FOOTSIES_NO_MALLOPT="1")
+    off = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True, env=env).stdout.split()
+    assert off == ["False", "False"]
