@@ -1462,8 +1462,8 @@ __device__ __forceinline__ void policy_features(const Lane& L, uint32_t& d0, uin
   d1 = pack_bf16x2((float)mf * (1.0f / 55.0f), L.f.x * (1.0f / 4.6f));
 }
 
-// One launch over all arenas, `TICKS` = 1 (k_step, the per-step VectorEnv path) or
-// p.n_steps (k_step_n*, the fused rollout: state stays in registers between ticks).
+// One fused launch over all arenas (k_step_n*, the rollout: state stays in registers between the
+// p.n_steps ticks); the one-tick launch is step_one below.
 // HASH draws the actions in-kernel from splitmix64 instead of reading action rows.
 // POL samples P1's action every tick from the MLP actor (fs_policy.h); its MFMAs and lane
 // exchanges need the whole wave, so lanes past the last arena stay in the loop (on a copy
@@ -1488,8 +1488,6 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     if constexpr (HASH) {
       return hash_action(p.action_seed, p.arena_base + (uint64_t)a, p.t0 + (uint64_t)t, k);
     } else {
-      if (!FUSED && p.inl_n)  // host inputs carried in the kernel arguments (fs_api.cpp)
-        return (p.inl[k][(uint32_t)a >> 2] >> (8u * ((uint32_t)a & 3u))) & 0xffu;
       return src[(uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a];
     }
   };
@@ -1517,10 +1515,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   } else {
     if (!active) return;
   }
-  if constexpr (!FUSED) {
-    if (p.active && !p.active[a]) return;  // fs_step_masked: this arena does not tick
-  }
-  L.ai = action_info<!FUSED>(L.f.act);
+  L.ai = action_info<false>(L.f.act);
   if constexpr (POL) {
     const uint32_t row_step = (uint32_t)p.out_stride_steps * (uint32_t)p.n_envs;
     const uint32_t arena0 = (uint32_t)(l & ~63) >> 1;
@@ -1582,16 +1577,72 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::"v"(a_fl), "v"(b_fl) : "memory");  // no load outlives the wave
     }
-  } else {
-    uint32_t none = 0;
-    env_step<FM, P2, -1, kTabGlobal>(L, next & 7u, p, (uint32_t)a, none);
   }
   if (active) store_lane<P2>(L, p.st, a);
 }
 
+// The one-tick launch (fs_step, fs_step_masked: the VectorEnv.step path).  Nothing is amortized
+// over ticks here, so the kernel is one dependent chain of memory round trips, and its prologue
+// is arranged to keep that chain short:
+// * every kernel argument the prologue needs is brought into SGPRs at once (one scalar-memory
+//   round trip; the compiler otherwise issued the state pointers' loads in two batches and the
+//   mask pointer's after the first vector loads had been waited for), and the block size is the
+//   launch constant kBlock rather than the dispatch packet's;
+// * the action row of the lane's player is selected between two SGPR pointers in registers (a
+//   per-lane `k ? p2 : p1` on the argument struct was compiled into a vector load of the pointer
+//   from the kernel-argument segment, waited for together with the state loads, before the
+//   action byte could be loaded), so the action byte, the mask byte and the arena state are in
+//   flight together;
+// * the tick's first table lookup, the ActionInfo of each fighter's action, comes from a copy of
+//   the 17-entry ActionInfo table that the wave's lanes 0-16 load alongside the state (lane j
+//   entry j) and a ds_bpermute by action index: an LDS-crossbar exchange instead of a dependent
+//   global-memory round trip after the state arrives.  Every lane is still active at that point
+//   (the exchange reads other lanes' registers), and lanes past the last arena leave after it.
+__device__ uint8_t kOneByte = 1;  // (global memory, so the select below stays a global load)
+template <int FM, int P2>
+__device__ __forceinline__ void step_one(const StepParams& p) {
+  const uint8_t* q1 = p.p1;
+  const uint8_t* q2 = p.p2;
+  const uint8_t* qm = p.active;
+  const int n_envs = p.n_envs, inl_n = p.inl_n;
+  // (inputs only: the pointers keep their global-memory provenance; and the two row pointers each
+  // have a use of their own here, so `k ? q2 : q1` stays a register select)
+  asm volatile("" ::"s"(p.st.pos), "s"(p.st.hist), "s"(p.st.fpk), "s"(p.st.aw), "s"(p.st.cum), "s"(q1), "s"(q2),
+               "s"(qm), "s"(n_envs), "s"(inl_n));
+  const int l = blockIdx.x * kBlock + threadIdx.x;
+  const bool active = l < 2 * n_envs;
+  const int a = active ? l >> 1 : 0;
+  const uint32_t k = l & 1;
+  // the two ActionInfo words the tick reads (frame count / loop start, cancel window), lane j of
+  // the wave holding action j's
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint2 tab = reinterpret_cast<const uint2*>(kTables.action)[2u * min(lane, (uint32_t)kNumActions - 1u)];
+  Lane L;
+  load_lane<P2>(L, p.st, a, k);
+  // this lane's input: host inputs in the kernel arguments (a few arenas), else its player's row
+  // (P1's unless a P1 bot plays; P2's when the handle has a remote P2)
+  const bool p2_rows = P2 == FS_P2_EXTERNAL || (P2 == kActors && !p.p2_noop && !p.p2_resets);
+  const bool reads = k == 0 ? !(P2 == kActors && p.p1_bot) : p2_rows;
+  const uint8_t* q = k == 0 ? q1 : q2;
+  uint32_t in = 0;
+  if (inl_n) in = (p.inl[k][(uint32_t)a >> 2] >> (8u * ((uint32_t)a & 3u))) & 0xffu;
+  else if (reads) in = q[a];
+  // fs_step_masked's byte, or a constant 1 (a load either way: no branch ahead of the state's use)
+  const uint32_t on = *(qm ? qm + a : &kOneByte);
+  // ActionInfo of the fighter's action, from lane L.f.act of this wave (all lanes active here)
+  const int src = L.f.act << 2;
+  L.ai.x = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)tab.x);
+  L.ai.y = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)tab.y);
+  L.ai.z = L.ai.w = 0u;  // (the cancel mask and padding: not read by the tick)
+  if (!active || !on) return;
+  uint32_t none = 0;
+  env_step<FM, P2, -1, kTabGlobal>(L, in & 7u, p, (uint32_t)a, none);
+  store_lane<P2>(L, p.st, a);
+}
+
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step(StepParams p) {
-  step_body<FM, P2, false, false>(p);
+  step_one<FM, P2>(p);
 }
 
 template <int FM, int P2>
