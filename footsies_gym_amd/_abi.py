@@ -41,6 +41,8 @@ FS_KERNEL_HASHED = 1
 FS_KERNEL_POLICY = 2
 FS_PPO_ACTOR_PARAMS = 5256
 FS_PPO_CRITIC_PARAMS = 4801
+FS_PPO_FP32 = 0
+FS_PPO_SPLIT_BF16 = 1
 
 # InputDefine (Assets/Script/InputData.cs:8-14)
 IN_LEFT, IN_RIGHT, IN_ATTACK = 1, 2, 4
@@ -153,6 +155,10 @@ LIB_FUNCTIONS = {
                               C.c_void_p, C.c_void_p, C.c_void_p]),
     "fs_ppo_grad": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp), C.c_float, C.c_float,
                               C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "fs_ppo_grad_ex": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp), C.c_float, C.c_float,
+                                 C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]),
+    "fs_ppo_eval_ex": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp),
+                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]),
     "fs_ppo_gae": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_float,
                              C.c_void_p, C.c_void_p, C.c_void_p]),
     "fs_ppo_features": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),

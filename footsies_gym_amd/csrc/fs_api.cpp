@@ -500,14 +500,16 @@ FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint
 
 FS_API size_t fs_ppo_workspace_bytes(void) { return fsk::ppo_workspace_bytes(); }
 
-FS_API int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
-                       float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
-                       size_t workspace_bytes, void* stream) {
+FS_API int fs_ppo_grad_ex(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
+                          float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
+                          size_t workspace_bytes, void* stream, int precision) {
   if (!rows || n <= 0 || !actor || !critic || !grad_out || !loss_out || !workspace)
     return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: rows, n > 0, both networks, outputs and workspace required");
   if (workspace_bytes < fsk::ppo_workspace_bytes())
     return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: workspace of %zu bytes, %zu needed", workspace_bytes,
                    fsk::ppo_workspace_bytes());
+  if (precision != FS_PPO_FP32 && precision != FS_PPO_SPLIT_BF16)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: unknown precision %d", precision);
   if (reinterpret_cast<uintptr_t>(rows) % 16)
     return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: rows must be 16-byte aligned");
   const float* const a[6] = {actor->w1, actor->b1, actor->w2, actor->b2, actor->w3, actor->b3};
@@ -515,19 +517,32 @@ FS_API int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const 
   for (int i = 0; i < 6; ++i)
     if (!a[i] || !c[i]) return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: all six arrays of each network required");
   const hipError_t e = fsk::launch_ppo_grad(rows, n, a, c, clip, vf_coef, ent_coef, grad_out, loss_out, workspace,
-                                            static_cast<hipStream_t>(stream));
+                                            static_cast<hipStream_t>(stream), precision == FS_PPO_SPLIT_BF16);
   if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_grad: %s", hipGetErrorString(e));
   return FS_OK;
 }
 
-FS_API int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp, const fs_mlp* actor,
-                       const fs_mlp* critic, float* values_out, float* logp_out, void* stream) {
+FS_API int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
+                       float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  return fs_ppo_grad_ex(rows, n, actor, critic, clip, vf_coef, ent_coef, grad_out, loss_out, workspace,
+                        workspace_bytes, stream, FS_PPO_FP32);
+}
+
+FS_API int fs_ppo_eval_ex(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp,
+                          const fs_mlp* actor, const fs_mlp* critic, float* values_out, float* logp_out,
+                          void* workspace, size_t workspace_bytes, void* stream, int precision) {
   if (!x || n_values <= 0 || n_logp < 0 || n_logp > n_values)
     return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: x, n_values > 0 and 0 <= n_logp <= n_values required");
   if (reinterpret_cast<uintptr_t>(x) % 16) return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: x must be 16-byte aligned");
   if (values_out && !critic) return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: values_out needs the critic");
   if (logp_out && n_logp > 0 && (!actor || !actions))
     return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: logp_out needs the actor and actions");
+  if (precision != FS_PPO_FP32 && precision != FS_PPO_SPLIT_BF16)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: unknown precision %d", precision);
+  if (precision == FS_PPO_SPLIT_BF16 && (!workspace || workspace_bytes < fsk::ppo_workspace_bytes()))
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: split-bf16 needs a workspace of %zu bytes",
+                   fsk::ppo_workspace_bytes());
   const fs_mlp none{};
   const fs_mlp& A = actor ? *actor : none;
   const fs_mlp& Cn = critic ? *critic : none;
@@ -536,10 +551,16 @@ FS_API int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions,
   for (int i = 0; i < 6; ++i)
     if ((values_out && !c[i]) || (logp_out && n_logp > 0 && !a[i]))
       return set_err(nullptr, FS_E_INVALID, "fs_ppo_eval: all six arrays of each network used required");
-  const hipError_t e = fsk::launch_ppo_eval(x, n_values, actions, n_logp, a, c, values_out, logp_out,
-                                            static_cast<hipStream_t>(stream));
+  const hipError_t e = fsk::launch_ppo_eval(x, n_values, actions, n_logp, a, c, values_out, logp_out, workspace,
+                                            static_cast<hipStream_t>(stream), precision == FS_PPO_SPLIT_BF16);
   if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_eval: %s", hipGetErrorString(e));
   return FS_OK;
+}
+
+FS_API int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp, const fs_mlp* actor,
+                       const fs_mlp* critic, float* values_out, float* logp_out, void* stream) {
+  return fs_ppo_eval_ex(x, n_values, actions, n_logp, actor, critic, values_out, logp_out, nullptr, 0, stream,
+                        FS_PPO_FP32);
 }
 
 FS_API int fs_ppo_gae(const double* rewards, const uint8_t* done, const float* values, int T, int64_t N, float gamma,

@@ -85,6 +85,7 @@ struct StepParams {
   int p1_bot;     // kActors: P1 is the bot (FS_P1_BOT)
   int p2_resets;  // kActors: P2's bot is Reset at Intro (the handle was created with FS_P2_BOT)
   int p2_noop;    // kActors: a non-bot P2 presses nothing (FS_P2_NOOP handle)
+  int prio;       // fused launches: time-sliced wave priority (set by the launcher, prio_slice)
   // host actions of a one-tick launch over at most kInlineArenas arenas, carried in the kernel
   // arguments instead of a staging copy (inl_n != 0): byte a of inl[player] is arena a's input
   int inl_n;
@@ -138,10 +139,10 @@ hipError_t launch_pack_records(const DevOutputs& o, void* dst, int n, hipStream_
 size_t ppo_workspace_bytes();
 hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
                            float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
-                           hipStream_t s);
+                           hipStream_t s, bool split);
 hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp,
                            const float* const actor[6], const float* const critic[6], float* values, float* logp,
-                           hipStream_t s);
+                           void* workspace, hipStream_t s, bool split);
 hipError_t launch_ppo_gae(const double* rew, const uint8_t* done, const float* val, int T, int64_t N, float gamma,
                           float gamma_lam, float* adv, float* ret, hipStream_t s);
 hipError_t launch_ppo_features(const uint8_t* guard, const uint8_t* move, const float* move_frame,

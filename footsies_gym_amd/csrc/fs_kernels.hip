@@ -1295,7 +1295,10 @@ __device__ __forceinline__ void settle_w(uint32_t& next) {
 // 20-tick one).  Every tick each wave raises its priority in alternate 2^9 / 100 MHz = 5.1 us
 // slices of the constant clock all CUs share, the two waves of a SIMD (wave slots of opposite
 // parity) in opposite slices, so both progress at the same rate and finish together.
-// (+4.8 % at 1000 ticks per launch, +3.4 % at 20; slices of 0.64 us: +0.4 %.)
+// (+4.8 % at 1000 ticks per launch, +3.4 % at 20; slices of 0.64 us: +0.4 %.)  With one wave per
+// SIMD there is nothing to balance and the clock read only lengthens the lone wave's tick (-3.5 %
+// at 32 768 arenas, profiles/r04d_ab32k.txt), so the launcher sets StepParams::prio only when the
+// grid holds more waves than the device has SIMDs.
 constexpr int kPrioSliceShift = 9;
 __device__ __forceinline__ uint32_t prio_group() {
   return __builtin_amdgcn_s_getreg(4 /* HW_ID */ | (31 << 11)) & 1u;  // bit 0 of the wave slot
@@ -1526,7 +1529,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
     for (int t = 0; t < p.n_steps; t++) {
       const uint32_t act = next;
       next = fetch(min(t + 1, p.n_steps - 1));
-      prio_slice(grp);
+      if (p.prio) prio_slice(grp);
       const PolicyOut po = policy_act(W, d0, d1, p.pol.seed, p.arena_base + arena0, p.t0 + (uint64_t)t);
       if (active) {
         const uint32_t row = (uint32_t)t * (uint32_t)p.n_envs + (uint32_t)a;
@@ -1545,7 +1548,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       for (int t = 0; t < p.n_steps; t++) {
         const uint32_t act = next;
         next = fetch(min(t + 1, p.n_steps - 1));
-        prio_slice(grp);
+        if (p.prio) prio_slice(grp);
         env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
       }
     } else {
@@ -1562,11 +1565,11 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       int t = 0;
       for (; t < last; t += 2) {
         a_fl = issue(t + 2);
-        prio_slice(grp);
+        if (p.prio) prio_slice(grp);
         env_step<FM, P2, 11>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
         b_rd = b_fl;
         b_fl = issue(t + 3);
-        prio_slice(grp);
+        if (p.prio) prio_slice(grp);
         env_step<FM, P2, 11>(L, reads ? b_rd & 7u : 0u, p, (uint32_t)(t + 1) * row_step + (uint32_t)a, a_fl);
         a_rd = a_fl;
       }
@@ -1931,9 +1934,23 @@ static bool fused_one_lane(int n_envs) {
   return n_envs >= threshold;
 }
 
+// Whether a two-lane fused launch over n_envs arenas holds more than one wave per SIMD, the case
+// prio_slice is for.  FOOTSIES_PRIO=0 / 1 forces it off / on (A/B timing).
+static bool two_waves_per_simd(int n_envs) {
+  static const int forced = [] {
+    const char* e = getenv("FOOTSIES_PRIO");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' + 1 : 0;
+  }();
+  if (forced) return forced == 2;
+  static const int simds = simd_count();
+  return (2 * (int64_t)n_envs + 63) / 64 > simds;
+}
+
 template <int FM, int P2>
-static void launch_step_p2(const StepParams& p, hipStream_t s) {
-  const dim3 grid = grid_for(2 * p.n_envs), block(kBlock);
+static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
+  const dim3 grid = grid_for(2 * p_in.n_envs), block(kBlock);
+  StepParams p = p_in;
+  p.prio = two_waves_per_simd(p.n_envs);
   if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
   else if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);

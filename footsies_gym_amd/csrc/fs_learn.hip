@@ -64,6 +64,39 @@ typedef float F4 __attribute__((ext_vector_type(4)));  // a 16 x 16 f32 MFMA acc
 __device__ __forceinline__ F4 mfma16(float a, float b, F4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+// Split-bf16 products (the opt-in FS_PPO_SPLIT_BF16 precision): each fp32 operand x of the three
+// 64-wide GEMMs is the pair hi = bf16(x), lo = bf16(x - hi) (x - hi is exact in fp32, so hi + lo
+// keeps 16 significant bits), and a product is hi.hi + hi.lo + lo.hi on
+// v_mfma_f32_32x32x16_bf16 with fp32 accumulation: lo.lo and the rounding of lo are below
+// 2^-15 of the product.  One 32x32x16 bf16 MFMA holds the pipe 32 cycles against the fp32
+// 32x32x2's 64, for 8x the K, so a K = 64 block costs 12 instead of 32 MFMAs of pipe time 384
+// instead of 2048 cycles.  Operand map (fs_policy.h, checked on the GPU by tools/mfma_probe):
+// lane l, r = l & 31, h = l >> 5 holds A[row r][k = 8h + j] and B[k = 8h + j][col r] in element j;
+// the 32 x 32 accumulator is laid out as the fp32 32x32x2's (col r, row (q & 3) + 8 (q >> 2) + 4h).
+typedef __bf16 BF8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ F16 mfma_bf16(BF8 a, BF8 b, F16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void split8(const float (&x)[8], BF8& hi, BF8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = (__bf16)x[j];
+    lo[j] = (__bf16)(x[j] - (float)hi[j]);
+  }
+}
+// the three products of one K = 16 step, the small ones first
+__device__ __forceinline__ F16 mfma_split(BF8 ah, BF8 al, BF8 bh, BF8 bl, F16 c) {
+  c = mfma_bf16(ah, bl, c);
+  c = mfma_bf16(al, bh, c);
+  return mfma_bf16(ah, bh, c);
+}
+// The weight fragments of the two 64-wide GEMMs with W2 as the A operand, built once per call by
+// k_ppo_frag: [mat: 0 = W2, 1 = W2^T][row block][k step][0 = hi, 1 = lo][lane] of 8 bf16 (16 B).
+constexpr int kFragsPerNet = 2 * 2 * 4 * 2 * 64;
+__device__ __forceinline__ int frag_at(int mat, int blk, int s, int part, int lane) {
+  return (((mat * 2 + blk) * 4 + s) * 2 + part) * 64 + lane;
+}
+
 // tanh without branches (the library tanhf runs both of its branches under divergence, ~30
 // instructions): |x| < 0.625 the same odd polynomial, above it 1 - 2 / (2^(2|x| log2 e) + 1)
 // with the hardware exp2 and reciprocal (within a few ulp of tanhf; 2^+inf -> 1 exactly).
@@ -157,14 +190,15 @@ __device__ __forceinline__ void store_rows_tanh(float* dst, const F16& v, int hf
 
 // EVAL: the forward pass only (fs_ppo_eval), rows = x [n][8]; the critic writes v per row into
 // out, the actor log_softmax(logits)[actions[row]].  Otherwise the gradient, rows [n][12].
-template <int OUT, bool EVAL = false>
+template <int OUT, bool EVAL = false, bool SPLIT = false>
 __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict__ rows, int64_t n, int64_t tiles,
                                                          const float* __restrict__ w1, const float* __restrict__ b1,
                                                          const float* __restrict__ w2, const float* __restrict__ b2,
                                                          const float* __restrict__ w3, const float* __restrict__ b3,
                                                          Coef c, float* __restrict__ partial,
                                                          const uint8_t* __restrict__ actions = nullptr,
-                                                         const float* __restrict__ w2t = nullptr) {
+                                                         const float* __restrict__ w2t = nullptr,
+                                                         const uint4* __restrict__ frags = nullptr) {
   constexpr int kStride = EVAL ? kF : kRow;
   __shared__ float sX[kTile][kF];
   __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample, then g1
@@ -226,7 +260,27 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 
     // ---- layer 2 on MFMA: H2^T[j][s] = b2[j] + sum_k W2[j][k] H1[s][k]; K = 64 as 32 steps of
     // (k = t, t + 32): A = W2[32 jb + r][t + 32 hf] (row loads), B = H1[r][t + 32 hf] (LDS row) ----
-    {
+    if constexpr (SPLIT) {  // K = 64 as 4 bf16 steps: B = H1[r][16 s + 8 hf + j], split per step
+      BF8 bh[4], bl[4];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const float4 v0 = *reinterpret_cast<const float4*>(&sH1[r][16 * st + 8 * hf]);
+        const float4 v1 = *reinterpret_cast<const float4*>(&sH1[r][16 * st + 8 * hf + 4]);
+        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        split8(v, bh[st], bl[st]);
+      }
+#pragma unroll 1
+      for (int jb = 0; jb < 2; ++jb) {  // (one block's fragments live at a time)
+        F16 acc = bias_frag(b2v + 32 * jb, hf);
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const BF8 ah = __builtin_bit_cast(BF8, frags[frag_at(0, jb, st, 0, lane)]);
+          const BF8 al = __builtin_bit_cast(BF8, frags[frag_at(0, jb, st, 1, lane)]);
+          acc = mfma_split(ah, al, bh[st], bl[st], acc);
+        }
+        store_rows_tanh(&sH2[r][32 * jb], acc, hf);
+      }
+    } else {
       float hb[32];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -403,6 +457,32 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 
     // ---- dW2[i][k] += sum_s G2[s][i] H1[s][k] on MFMA: K = the tile's samples as 16 steps of
     // (s = t, t + 16): A = G2[t + 16 hf][32 ib + r], B = H1[t + 16 hf][32 kb + r]; db2 alongside ---
+    if constexpr (SPLIT) {  // K = 32 samples as 2 bf16 steps of samples 16 st + 8 hf + j
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        BF8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = sH2[16 * st + 8 * hf + j][32 * ib + r];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dB2[ib] += v[j];
+          split8(v, ah[ib], al[ib]);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = sH1[16 * st + 8 * hf + j][32 * kb + r];
+          split8(v, bh[kb], bl[kb]);
+        }
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) dW2[ib][kb] = mfma_split(ah[ib], al[ib], bh[kb], bl[kb], dW2[ib][kb]);
+      }
+    } else {
 #pragma unroll
     for (int t = 0; t < kTile / 2; ++t) {
       const int sidx = t + (kTile / 2) * hf;
@@ -415,11 +495,40 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       dW2[1][0] = mfma32(a1, h0, dW2[1][0]);
       dW2[1][1] = mfma32(a1, h1v, dW2[1][1]);
     }
+    }
     __syncthreads();
 
     // ---- backward through W2 on MFMA: gh1^T[i][s] = sum_j W2[j][i] G2[s][j] (A = W2[t + 32 hf][32 ib
     // + r], B = G2[r][t + 32 hf]); g1 = gh1 (1 - h1^2) overwrites h1 where this lane read it ---------
-    {
+    if constexpr (SPLIT) {  // A = W2^T[32 ib + r][16 s + 8 hf + j] fragments, B = G2[r][16 s + 8 hf + j]
+      BF8 gh[4], gl[4];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const float4 v0 = *reinterpret_cast<const float4*>(&sH2[r][16 * st + 8 * hf]);
+        const float4 v1 = *reinterpret_cast<const float4*>(&sH2[r][16 * st + 8 * hf + 4]);
+        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        split8(v, gh[st], gl[st]);
+      }
+#pragma unroll 1
+      for (int ib = 0; ib < 2; ++ib) {  // (one block's fragments live at a time)
+        F16 acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const BF8 ah = __builtin_bit_cast(BF8, frags[frag_at(1, ib, st, 0, lane)]);
+          const BF8 al = __builtin_bit_cast(BF8, frags[frag_at(1, ib, st, 1, lane)]);
+          acc = mfma_split(ah, al, gh[st], gl[st], acc);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {  // rows i = 32 ib + 8 qq + 4 hf + (0..3) of sample r
+          float4* hp = reinterpret_cast<float4*>(&sH1[r][32 * ib + 8 * qq + 4 * hf]);
+          const float4 hv = *hp;
+          *hp = make_float4(acc[4 * qq] * (1.f - hv.x * hv.x), acc[4 * qq + 1] * (1.f - hv.y * hv.y),
+                            acc[4 * qq + 2] * (1.f - hv.z * hv.z), acc[4 * qq + 3] * (1.f - hv.w * hv.w));
+        }
+      }
+    } else {
       float gb[32];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -502,6 +611,29 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     out[n_params<OUT>() + 1] = vf_sum;
     out[n_params<OUT>() + 2] = ent_sum;
   }
+}
+
+// The split-bf16 A fragments of both networks (k_ppo_grad<., ., true>): for mat 0, W2[32 blk + r][16 s
+// + 8 h + j]; for mat 1, W2^T[32 blk + r][...] = W2[16 s + 8 h + j][32 blk + r]; hi = bf16(w),
+// lo = bf16(w - hi).  One thread per (net, mat, blk, s, lane).
+__global__ __launch_bounds__(256) void k_ppo_frag(const float* __restrict__ wa, const float* __restrict__ wc,
+                                                 uint4* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;  // < 2 nets x 2 mats x 2 blks x 4 steps x 64 lanes
+  if (t >= 2 * 2 * 2 * 4 * 64) return;
+  const int lane = t & 63, s = (t >> 6) & 3, blk = (t >> 8) & 1, mat = (t >> 9) & 1, net = t >> 10;
+  const float* w = net ? wc : wa;
+  const int r = lane & 31, h = lane >> 5;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = 32 * blk + r, k = 16 * s + 8 * h + j;
+    v[j] = mat == 0 ? w[row * kH + k] : w[k * kH + row];
+  }
+  BF8 hi, lo;
+  split8(v, hi, lo);
+  uint4* o = out + net * kFragsPerNet;
+  o[frag_at(mat, blk, s, 0, lane)] = __builtin_bit_cast(uint4, hi);
+  o[frag_at(mat, blk, s, 1, lane)] = __builtin_bit_cast(uint4, lo);
 }
 
 // W2^T of both networks into the workspace (64 x 64 each), so the backward pass through W2 reads
@@ -626,14 +758,16 @@ hipError_t launch_ppo_pack(const float* x, const uint8_t* act, const float* old,
   return hipGetLastError();
 }
 
-size_t ppo_workspace_bytes() {
+// workspace: the actor's and the critic's partial gradients, W2^T of both, the split-bf16 fragments
+static size_t ppo_frag_offset() {
   return sizeof(float) * ((size_t)fsl::kMaxWaves * (fsl::partial_stride<8>() + fsl::partial_stride<1>()) +
                           2 * fsl::kH * fsl::kH);
 }
+size_t ppo_workspace_bytes() { return ppo_frag_offset() + sizeof(uint4) * 2 * fsl::kFragsPerNet; }
 
 hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
                            float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
-                           hipStream_t s) {
+                           hipStream_t s, bool split) {
   using namespace fsl;
   const int64_t tiles = (n + kTile - 1) / kTile;
   const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
@@ -641,13 +775,22 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
   float* pa = static_cast<float*>(workspace);
   float* pc = pa + (size_t)kMaxWaves * partial_stride<8>();
   float* w2t = pc + (size_t)kMaxWaves * partial_stride<1>();  // [2][64][64]: actor, critic
+  uint4* frags = reinterpret_cast<uint4*>(static_cast<char*>(workspace) + ppo_frag_offset());
   hipError_t e = hipMemsetAsync(loss, 0, 3 * sizeof(float), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_ppo_t64, dim3(4, 2), dim3(256), 0, s, actor[2], critic[2], w2t);
-  hipLaunchKernelGGL(k_ppo_grad<8>, dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1], actor[2],
-                     actor[3], actor[4], actor[5], c, pa, nullptr, w2t);
-  hipLaunchKernelGGL(k_ppo_grad<1>, dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1], critic[2],
-                     critic[3], critic[4], critic[5], c, pc, nullptr, w2t + kH * kH);
+  if (split) {
+    hipLaunchKernelGGL(k_ppo_frag, dim3(8), dim3(256), 0, s, actor[2], critic[2], frags);
+    hipLaunchKernelGGL((k_ppo_grad<8, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1],
+                       actor[2], actor[3], actor[4], actor[5], c, pa, nullptr, nullptr, frags);
+    hipLaunchKernelGGL((k_ppo_grad<1, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1],
+                       critic[2], critic[3], critic[4], critic[5], c, pc, nullptr, nullptr, frags + kFragsPerNet);
+  } else {
+    hipLaunchKernelGGL(k_ppo_t64, dim3(4, 2), dim3(256), 0, s, actor[2], critic[2], w2t);
+    hipLaunchKernelGGL(k_ppo_grad<8>, dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1], actor[2],
+                       actor[3], actor[4], actor[5], c, pa, nullptr, w2t);
+    hipLaunchKernelGGL(k_ppo_grad<1>, dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1], critic[2],
+                       critic[3], critic[4], critic[5], c, pc, nullptr, w2t + kH * kH);
+  }
   hipLaunchKernelGGL(k_ppo_reduce<8>, dim3((n_params<8>() + 3 + 63) / 64), dim3(1024), 0, s, pa, waves, grad, loss,
                      c.inv_n);
   hipLaunchKernelGGL(k_ppo_reduce<1>, dim3((n_params<1>() + 3 + 63) / 64), dim3(1024), 0, s, pc, waves,
@@ -657,20 +800,36 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
 
 hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp,
                            const float* const actor[6], const float* const critic[6], float* values, float* logp,
-                           hipStream_t s) {
+                           void* workspace, hipStream_t s, bool split) {
   using namespace fsl;
   const Coef c{0.f, 0.f, 0.f, 0.f};
-  if (values && n_values > 0) {
+  uint4* frags = split ? reinterpret_cast<uint4*>(static_cast<char*>(workspace) + ppo_frag_offset()) : nullptr;
+  const bool run_v = values && n_values > 0, run_l = logp && n_logp > 0;
+  if (split) {  // (a network not run passes its actor / critic arrays as null: its fragments are not built)
+    const float* wa = run_l ? actor[2] : (run_v ? critic[2] : nullptr);
+    const float* wc = run_v ? critic[2] : wa;
+    if (wa) hipLaunchKernelGGL(k_ppo_frag, dim3(8), dim3(256), 0, s, wa, wc, frags);
+  }
+  if (run_v) {
     const int64_t tiles = (n_values + kTile - 1) / kTile;
     const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
-    hipLaunchKernelGGL((k_ppo_grad<1, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, critic[0], critic[1],
-                       critic[2], critic[3], critic[4], critic[5], c, values, nullptr);
+    if (split)
+      hipLaunchKernelGGL((k_ppo_grad<1, true, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, critic[0],
+                         critic[1], critic[2], critic[3], critic[4], critic[5], c, values, nullptr, nullptr,
+                         frags + kFragsPerNet);
+    else
+      hipLaunchKernelGGL((k_ppo_grad<1, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, critic[0], critic[1],
+                         critic[2], critic[3], critic[4], critic[5], c, values, nullptr);
   }
-  if (logp && n_logp > 0) {
+  if (run_l) {
     const int64_t tiles = (n_logp + kTile - 1) / kTile;
     const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
-    hipLaunchKernelGGL((k_ppo_grad<8, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, actor[0], actor[1],
-                       actor[2], actor[3], actor[4], actor[5], c, logp, actions);
+    if (split)
+      hipLaunchKernelGGL((k_ppo_grad<8, true, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, actor[0],
+                         actor[1], actor[2], actor[3], actor[4], actor[5], c, logp, actions, nullptr, frags);
+    else
+      hipLaunchKernelGGL((k_ppo_grad<8, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, actor[0], actor[1],
+                         actor[2], actor[3], actor[4], actor[5], c, logp, actions);
   }
   return hipGetLastError();
 }

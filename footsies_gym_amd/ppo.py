@@ -111,10 +111,21 @@ class PPOGrad:
     """fs_ppo_grad for an actor (8-64-64-8) and a critic (8-64-64-1): each call writes the
     minibatch gradient of PPO's loss into one flat device buffer whose views are the
     parameters' ``.grad`` (set once here), and returns the device [3] of (policy, value,
-    entropy) loss means."""
+    entropy) loss means.
 
-    def __init__(self, actor, critic):
+    precision: "fp32" (default) runs the 64x64 hidden layer on fp32 FMAs; "split_bf16"
+    (FS_PPO_SPLIT_BF16) runs it on bf16 MFMAs with each fp32 operand split into a bf16 high
+    and low part (hi*hi + hi*lo + lo*hi, fp32 accumulation: ~2^-16 relative per product) --
+    same results to ~1e-5 relative, not bit-identical to the fp32 path."""
+
+    PRECISIONS = {"fp32": _abi.FS_PPO_FP32, "split_bf16": _abi.FS_PPO_SPLIT_BF16}
+
+    def __init__(self, actor, critic, precision="fp32"):
         torch = _torch()
+        if precision not in self.PRECISIONS:
+            raise ValueError("precision must be one of %s" % sorted(self.PRECISIONS))
+        self.precision = precision
+        self._prec = self.PRECISIONS[precision]
         self._modules = (actor, critic)
         nets = self._collect()
         dev = nets[0][0].device
@@ -199,9 +210,11 @@ class PPOGrad:
             logp = torch.empty(n_logp, dtype=torch.float32, device=x.device)
         self._check_bindings()
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        check(lib().fs_ppo_eval(C.c_void_p(x.data_ptr()), n, C.c_void_p(actions.data_ptr() if n_logp else None),
-                                n_logp, C.byref(self._mlps[0]), C.byref(self._mlps[1]), C.c_void_p(values.data_ptr()),
-                                C.c_void_p(logp.data_ptr() if n_logp else None), C.c_void_p(stream)))
+        check(lib().fs_ppo_eval_ex(C.c_void_p(x.data_ptr()), n, C.c_void_p(actions.data_ptr() if n_logp else None),
+                                   n_logp, C.byref(self._mlps[0]), C.byref(self._mlps[1]),
+                                   C.c_void_p(values.data_ptr()), C.c_void_p(logp.data_ptr() if n_logp else None),
+                                   C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), C.c_void_p(stream),
+                                   self._prec))
         return values, logp
 
     def __call__(self, rows, clip, vf_coef, ent_coef):
@@ -211,10 +224,10 @@ class PPOGrad:
             raise ValueError("rows must be a contiguous [n, 12] float32 tensor")
         self._check_bindings()
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        check(lib().fs_ppo_grad(C.c_void_p(rows.data_ptr()), rows.shape[0], C.byref(self._mlps[0]),
-                                C.byref(self._mlps[1]), clip, vf_coef, ent_coef, C.c_void_p(self.grad.data_ptr()),
-                                C.c_void_p(self.loss.data_ptr()), C.c_void_p(self.workspace.data_ptr()),
-                                self.workspace.numel(), C.c_void_p(stream)))
+        check(lib().fs_ppo_grad_ex(C.c_void_p(rows.data_ptr()), rows.shape[0], C.byref(self._mlps[0]),
+                                   C.byref(self._mlps[1]), clip, vf_coef, ent_coef, C.c_void_p(self.grad.data_ptr()),
+                                   C.c_void_p(self.loss.data_ptr()), C.c_void_p(self.workspace.data_ptr()),
+                                   self.workspace.numel(), C.c_void_p(stream), self._prec))
         return self.loss
 
 
@@ -296,7 +309,7 @@ class PPOTrainer:
 
     def __init__(self, sim, actor=None, critic=None, horizon=128, gamma=0.99, lam=0.95, epochs=2, minibatches=4,
                  lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour", learner="hip",
-                 kl_ticks=None):
+                 kl_ticks=None, learner_precision="fp32"):
         torch = _torch()
         if old_logp not in ("behaviour", "fp32"):
             raise ValueError("old_logp must be 'behaviour' or 'fp32'")
@@ -320,7 +333,7 @@ class PPOTrainer:
         # one fused kernel per step on the device instead of ~7 foreach launches
         self.opt = torch.optim.Adam(list(self.actor.parameters()) + list(self.critic.parameters()), lr=lr,
                                     fused=dev.type == "cuda")
-        self._grad = PPOGrad(self.actor, self.critic) if learner == "hip" else None
+        self._grad = PPOGrad(self.actor, self.critic, precision=learner_precision) if learner == "hip" else None
         self.traj = sim.alloc_trajectory(horizon)
         n = sim.num_envs
         self.actions = torch.empty((horizon, n), dtype=torch.uint8, device=dev)

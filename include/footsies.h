@@ -306,6 +306,21 @@ int fs_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_
 int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
                 float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
                 size_t workspace_bytes, void* stream);
+/* The same two calls with the precision of the three 64-wide products (layer 2's forward pass,
+ * the backward pass through W2 and dW2) chosen: FS_PPO_FP32 (fs_ppo_grad / fs_ppo_eval: fp32
+ * MFMA, exact fp32 products) or FS_PPO_SPLIT_BF16 (each fp32 operand split into a bf16 hi + lo
+ * pair and the product taken as hi.hi + hi.lo + lo.hi on bf16 MFMA with fp32 accumulation:
+ * relative error per product below 2^-15, ~5x less matrix-pipe time).  The layers with 8 inputs
+ * or outputs stay fp32.  fs_ppo_eval_ex needs the workspace for FS_PPO_SPLIT_BF16 (NULL / 0 for
+ * FS_PPO_FP32); a workspace is not shared between calls in flight on different streams. */
+#define FS_PPO_FP32 0
+#define FS_PPO_SPLIT_BF16 1
+int fs_ppo_grad_ex(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
+                   float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
+                   size_t workspace_bytes, void* stream, int precision);
+int fs_ppo_eval_ex(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp, const fs_mlp* actor,
+                   const fs_mlp* critic, float* values_out, float* logp_out, void* workspace, size_t workspace_bytes,
+                   void* stream, int precision);
 /* GAE of a [T][N] trajectory (ppo.py gae), asynchronously on `stream`: rewards device
  * [T][N] f64 and done device [T][N] u8 as fs_step_n_policy's trajectory holds them, values
  * device [T + 1][N] f32 (the last row bootstraps); delta = (r + (gamma v[t+1]) keep) - v[t],

@@ -1,17 +1,22 @@
 """fs_ppo_grad (csrc/fs_learn.hip), the C5 learner's fused forward + backward, against torch
 autograd on the same loss (ppo.py's learner="torch" path, written out here): fp32 gradients of
 both networks and the three loss means, on ragged sample counts (a partial last 64-sample
-tile), with ratios inside and outside the clip range and a zero-advantage tie.
+tile), with ratios inside and outside the clip range and a zero-advantage tie.  Both learner
+precisions: "fp32" (fp32 FMAs) and the opt-in "split_bf16" (hidden layer on bf16 MFMAs with
+each fp32 operand split hi + lo).
 
 Tolerance: the kernel and hipBLASLt sum in different orders in fp32, so each gradient tensor
 must agree to rtol 1e-4 with atol 1e-6 x that tensor's largest magnitude (measured differences
-are ~1e-6 relative).  Not a bit-exact path: this is the learner beside the simulator."""
+are ~1e-6 relative).  split_bf16 drops the lo*lo term of every hidden-layer product (2^-16
+relative of it) before fp32 accumulation: the same rtol, atol 1e-5 x the largest magnitude.
+Not a bit-exact path: this is the learner beside the simulator."""
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-4
-ATOL_FRAC = 1e-6
+ATOL_FRAC = {"fp32": 1e-6, "split_bf16": 1e-5}
+PRECISIONS = ("fp32", "split_bf16")
 
 
 def _nets(seed):
@@ -22,8 +27,12 @@ def _nets(seed):
     return make_actor(device=dev, seed=seed), make_critic(device=dev, seed=seed + 1)
 
 
-def _rows(actor, n, seed):
-    """[n, 12] rows whose old log-probs put ratios below, inside and above the clip range."""
+def _rows(actor, n, seed, margin=1e-3, clip=0.2):
+    """[n, 12] rows whose old log-probs put ratios below, inside and above the clip range, none
+    within `margin` of a clip edge: there the clipped loss's gradient jumps (the sample's policy
+    term switches on or off), so any rounding difference in the forward pass can flip a sample
+    and move the minibatch gradient by ~1/sqrt(n) relative -- a property of the loss, not of
+    the kernel (measured with the float64 reference: tools/split_error.py)."""
     import torch
     g = torch.Generator(device="cuda").manual_seed(seed)
     dev = torch.device("cuda", 0)
@@ -32,6 +41,9 @@ def _rows(actor, n, seed):
     with torch.no_grad():
         lp = torch.log_softmax(actor(x), dim=1).gather(1, a[:, None])[:, 0]
     old = lp + torch.randn(n, generator=g, device=dev) * 0.3
+    for edge in (1 - clip, 1 + clip):  # ratio = exp(lp - old): move old so it sits 2 margins away
+        near = (torch.exp(lp - old) - edge).abs() < margin
+        old = torch.where(near, lp - torch.log(torch.full_like(old, edge + 2 * margin)), old)
     adv = torch.randn(n, generator=g, device=dev)
     adv[::17] = 0.0  # s1 == s2 == 0: torch.min's tie
     ret = torch.randn(n, generator=g, device=dev)
@@ -59,15 +71,16 @@ def _torch_reference(actor, critic, rows, clip, vf_coef, ent_coef):
     return grads, torch.stack([pg, vf, ent]).detach()
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("n", [1, 63, 64, 5000, 70001])
-def test_ppo_grad_matches_autograd(n):
+def test_ppo_grad_matches_autograd(n, precision):
     import torch
     from footsies_gym_amd.ppo import PPOGrad
     actor, critic = _nets(seed=n % 7)
     rows = _rows(actor, n, seed=n)
     clip, vf_coef, ent_coef = 0.2, 0.5, 0.01
     ref, ref_loss = _torch_reference(actor, critic, rows, clip, vf_coef, ent_coef)
-    pg = PPOGrad(actor, critic)
+    pg = PPOGrad(actor, critic, precision=precision)
     loss = pg(rows, clip, vf_coef, ent_coef).clone()
     got = [p.grad.detach().clone() for p in pg.params]
     torch.cuda.synchronize()
@@ -79,18 +92,20 @@ def test_ppo_grad_matches_autograd(n):
     for name, g, e in zip(names, got, ref):
         assert g.shape == e.shape, name
         scale = float(e.abs().max())
-        torch.testing.assert_close(g, e, rtol=RTOL, atol=ATOL_FRAC * max(scale, 1e-12), msg=name)
+        torch.testing.assert_close(g, e, rtol=RTOL, atol=ATOL_FRAC[precision] * max(scale, 1e-12),
+                                   msg=lambda m, name=name: name + ": " + m)
     torch.testing.assert_close(loss, ref_loss, rtol=RTOL, atol=1e-6)
 
 
-def test_ppo_grad_is_deterministic_and_rejects_bad_input():
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_ppo_grad_is_deterministic_and_rejects_bad_input(precision):
     import torch
     from footsies_gym_amd._lib import FootsiesError
     from footsies_gym_amd.ppo import PPOGrad
     from footsies_gym_amd.rollout import make_actor
     actor, critic = _nets(seed=2)
     rows = _rows(actor, 200_000, seed=9)
-    pg = PPOGrad(actor, critic)
+    pg = PPOGrad(actor, critic, precision=precision)
     pg(rows, 0.2, 0.5, 0.01)
     first = pg.grad.clone()
     pg(rows, 0.2, 0.5, 0.01)
@@ -101,6 +116,8 @@ def test_ppo_grad_is_deterministic_and_rejects_bad_input():
         pg(rows[:0], 0.2, 0.5, 0.01)
     with pytest.raises(ValueError):
         PPOGrad(make_actor(hidden=32, device=torch.device("cuda", 0)), critic)
+    with pytest.raises(ValueError):
+        PPOGrad(actor, critic, precision="bf16")
 
 
 def test_ppo_trainer_hip_step_equals_torch_step():
@@ -134,8 +151,9 @@ def test_ppo_trainer_hip_step_equals_torch_step():
     assert flips <= total // 1000, (flips, total)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("n,n_logp", [(1, 1), (100, 37), (70001, 70001), (131072 + 65536, 131072)])
-def test_ppo_eval_matches_torch_forward(n, n_logp):
+def test_ppo_eval_matches_torch_forward(n, n_logp, precision):
     """fs_ppo_eval: critic values of every row and the actor's log-probability of the taken action
     for the first n_logp rows, against the torch modules' forward pass (fp32, same tolerance)."""
     import torch
@@ -144,13 +162,13 @@ def test_ppo_eval_matches_torch_forward(n, n_logp):
     g = torch.Generator(device="cuda").manual_seed(n)
     x = (torch.rand((n, 8), generator=g, device="cuda") * 2 - 0.5).contiguous()
     a = torch.randint(0, 8, (n_logp,), generator=g, device="cuda").to(torch.uint8)
-    v, lp = PPOGrad(actor, critic).evaluate(x, a, n_logp)
+    v, lp = PPOGrad(actor, critic, precision=precision).evaluate(x, a, n_logp)
     with torch.no_grad():
         v_ref = critic(x).squeeze(-1)
         lp_ref = torch.log_softmax(actor(x[:n_logp]), 1).gather(1, a.long()[:, None])[:, 0]
     torch.testing.assert_close(v, v_ref, rtol=RTOL, atol=1e-5)
     torch.testing.assert_close(lp, lp_ref, rtol=RTOL, atol=1e-5)
-    v2, lp2 = PPOGrad(actor, critic).evaluate(x)
+    v2, lp2 = PPOGrad(actor, critic, precision=precision).evaluate(x)
     assert lp2 is None and torch.equal(v2, v)
 
 
@@ -235,3 +253,21 @@ def test_ppo_grad_follows_replaced_parameters():
     lin[0].bias = torch.nn.Parameter(lin[0].bias.detach().cpu())
     with pytest.raises(ValueError):
         pg(rows, 0.2, 0.5, 0.01)
+
+
+def test_split_bf16_eval_agrees_with_fp32_eval():
+    """The two precisions' forward passes on the same rows: values and log-probs within rtol 1e-4,
+    atol 5e-5 of each other (each hidden-layer product is off by up to ~3 x 2^-17 relative before
+    the sums; measured: 3.8e-5 absolute on log-probs near -2), and not identical (the MFMA path ran)."""
+    import torch
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=6)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    n = 20000
+    x = (torch.rand((n, 8), generator=g, device="cuda") * 2 - 0.5).contiguous()
+    a = torch.randint(0, 8, (n,), generator=g, device="cuda").to(torch.uint8)
+    v32, lp32 = PPOGrad(actor, critic).evaluate(x, a, n)
+    vs, lps = PPOGrad(actor, critic, precision="split_bf16").evaluate(x, a, n)
+    torch.testing.assert_close(vs, v32, rtol=1e-4, atol=5e-5)
+    torch.testing.assert_close(lps, lp32, rtol=1e-4, atol=5e-5)
+    assert not torch.equal(vs, v32) or not torch.equal(lps, lp32)

@@ -165,7 +165,8 @@ def test_fused_policy_without_outputs_and_bad_args():
 @pytest.mark.parametrize("N,horizon,iters,old,learner", [(2048, 32, 3, "behaviour", "hip"),
                                                          (2048, 32, 2, "fp32", "hip"),
                                                          (2048, 32, 2, "behaviour", "torch"),
-                                                         (65536, 16, 2, "behaviour", "hip")])
+                                                         (65536, 16, 2, "behaviour", "hip"),
+                                                         (2048, 32, 3, "behaviour", "hip_split_bf16")])
 def test_ppo_iterations_learn_and_refresh_the_kernel_actor(N, horizon, iters, old, learner):
     """PPOTrainer: fused rollouts + fused-kernel (or torch autograd) updates; losses finite, weights move, and the
     kernel samples from the refreshed weights (the same seed then draws different actions).
@@ -174,7 +175,9 @@ def test_ppo_iterations_learn_and_refresh_the_kernel_actor(N, horizon, iters, ol
     from footsies_gym_amd.ppo import PPOTrainer
     from footsies_gym_amd.simulator import FootsiesSim
     sim = FootsiesSim(N, p2_mode="bot", seed=5)
-    tr = PPOTrainer(sim, horizon=horizon, epochs=2, minibatches=4, lr=1e-2, seed=3, old_logp=old, learner=learner)
+    learner, prec = ("hip", "split_bf16") if learner == "hip_split_bf16" else (learner, "fp32")
+    tr = PPOTrainer(sim, horizon=horizon, epochs=2, minibatches=4, lr=1e-2, seed=3, old_logp=old, learner=learner,
+                    learner_precision=prec)
     w0 = [p.detach().clone() for p in tr.actor.parameters()]
     k0 = [p.clone() for p in tr.rollout.params]
     rate = tr.train(iters)

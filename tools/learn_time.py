@@ -1,6 +1,6 @@
 """Time one C5 minibatch gradient (65 536 arenas x 128 ticks / 4 minibatches = 2 097 152 rows):
-fs_ppo_grad (PPOGrad) against the same loss through torch autograd (ppo.py learner="torch",
-with its SkinnyLinear weight gradients).  Prints one JSON line."""
+fs_ppo_grad (PPOGrad) in both precisions against the same loss through torch autograd (ppo.py
+learner="torch", with its SkinnyLinear weight gradients), and fs_ppo_eval in both precisions.  Prints one JSON line."""
 import json
 import sys
 import time
@@ -20,9 +20,21 @@ def main(n=2_097_152, reps=10, only=None):
     a = torch.randint(0, 8, (n,), generator=g, device=dev).float()
     rows = torch.cat([x, a[:, None], torch.randn((n, 3), generator=g, device=dev) * 0.3], 1).contiguous()
     pg = PPOGrad(actor, critic)
+    ps = PPOGrad(actor, critic, precision="split_bf16")
+    xe = torch.rand((n + 65536, 8), generator=g, device=dev)
+    ae = torch.randint(0, 8, (n + 65536,), generator=g, device=dev).to(torch.uint8)
 
     def hip():
         pg(rows, 0.2, 0.5, 0.01)
+
+    def hip_split():
+        ps(rows, 0.2, 0.5, 0.01)
+
+    def eval_fp32():  # one update's forward passes: values of T + 1 ticks, log-probs of the first
+        pg.evaluate(xe, ae, n // 16)
+
+    def eval_split():
+        ps.evaluate(xe, ae, n // 16)
 
     def ref():
         xb, ab = rows[:, :8], rows[:, 8].long()
@@ -35,7 +47,8 @@ def main(n=2_097_152, reps=10, only=None):
         loss.backward()
 
     out = {"rows": n}
-    for name, fn in (("hip_ms", hip), ("torch_ms", ref)):
+    for name, fn in (("hip_ms", hip), ("hip_split_ms", hip_split), ("eval_fp32_ms", eval_fp32),
+                     ("eval_split_ms", eval_split), ("torch_ms", ref)):
         if only and not name.startswith(only):
             continue
         fn()
@@ -48,6 +61,9 @@ def main(n=2_097_152, reps=10, only=None):
     # 2 x (forward 5 120 + backward 4 608 + weight gradients 5 120) fp32 FMAs per row, roughly
     if "hip_ms" in out:
         out["hip_tflops"] = 2 * n * 2 * (5120 + 4608 + 5120) / (out["hip_ms"] * 1e-3) / 1e12
+    if "hip_split_ms" in out:
+        out["hip_split_speedup"] = out["hip_ms"] / out["hip_split_ms"]
+        out["eval_split_speedup"] = out["eval_fp32_ms"] / out["eval_split_ms"]
     print(json.dumps(out))
 
 
