@@ -230,21 +230,23 @@ def ppo_rate(torch, N, device, horizon=128, iterations=3):
     """Config C5 end to end: PPO iterations (fused rollout of `horizon` ticks with the in-kernel
     actor, then GAE and 2 epochs x 4 minibatches of fp32 Adam updates of actor and critic, then
     the new weights copied into the kernel's buffers); P2 = bot.  `value` with the fused
-    learner kernel (fs_ppo_grad), `split_bf16_learner` with its opt-in split-bf16 MFMA precision,
-    `torch_learner` with the same loss through torch autograd.  One untimed warm-up iteration each."""
+    learner kernel (fs_ppo_grad) at PPOTrainer's default split-bf16 precision, `fp32_learner`
+    with its fp32-FMA precision, `torch_learner` with the same loss through torch autograd.  One
+    untimed warm-up iteration each."""
     from footsies_gym_amd.ppo import PPOTrainer
     from footsies_gym_amd.simulator import FootsiesSim
     rates = {}
-    for key, learner, prec in (("hip", "hip", "fp32"), ("hip_split", "hip", "split_bf16"), ("torch", "torch", "fp32")):
+    for key, learner, prec in (("hip_split", "hip", "split_bf16"), ("hip", "hip", "fp32"), ("torch", "torch", "fp32")):
         sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0)
         tr = PPOTrainer(sim, horizon=horizon, learner=learner, learner_precision=prec)
         tr.train(1)
         rates[key] = tr.train(iterations)
         sim.close()
-    return {"value": rates["hip"], "split_bf16_learner": rates["hip_split"], "torch_learner": rates["torch"],
+    return {"value": rates["hip_split"], "fp32_learner": rates["hip"], "torch_learner": rates["torch"],
             "horizon": horizon, "iterations": iterations,
             "config": "C5 end to end: %d arenas, PPO (fused rollout of %d ticks + GAE + 2x4 Adam minibatch "
-                      "updates of the 8-64-64-8 actor and critic, gradients by fs_ppo_grad), P2 = bot"
+                      "updates of the 8-64-64-8 actor and critic, gradients by fs_ppo_grad with the split-bf16 "
+                      "hidden layer), P2 = bot"
                       % (N, horizon)}
 
 

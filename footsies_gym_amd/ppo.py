@@ -305,11 +305,14 @@ def pack_rows(x, actions, old, adv, ret, out=None):
 
 class PPOTrainer:
     """PPO over a FootsiesSim (P2 = whatever the sim was created with).  `horizon` ticks per
-    rollout, all arenas in every minibatch round."""
+    rollout, all arenas in every minibatch round.  `learner_precision` is PPOGrad's: the
+    split-bf16 hidden layer by default -- against a float64 autograd reference its gradients are
+    within 5e-6 of each tensor's largest entry, as close as torch's own fp32 autograd (up to
+    1.1e-5; profiles/r04e_split_error.jsonl) -- or "fp32"."""
 
     def __init__(self, sim, actor=None, critic=None, horizon=128, gamma=0.99, lam=0.95, epochs=2, minibatches=4,
                  lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour", learner="hip",
-                 kl_ticks=None, learner_precision="fp32"):
+                 kl_ticks=None, learner_precision="split_bf16"):
         torch = _torch()
         if old_logp not in ("behaviour", "fp32"):
             raise ValueError("old_logp must be 'behaviour' or 'fp32'")

@@ -1,9 +1,9 @@
 """fs_ppo_grad (csrc/fs_learn.hip), the C5 learner's fused forward + backward, against torch
 autograd on the same loss (ppo.py's learner="torch" path, written out here): fp32 gradients of
 both networks and the three loss means, on ragged sample counts (a partial last 64-sample
-tile), with ratios inside and outside the clip range and a zero-advantage tie.  Both learner
-precisions: "fp32" (fp32 FMAs) and the opt-in "split_bf16" (hidden layer on bf16 MFMAs with
-each fp32 operand split hi + lo).
+tile), with ratios inside and outside the clip range (none within 1e-3 of a clip edge, see
+_rows) and a zero-advantage tie.  Both learner precisions: "fp32" (fp32 FMAs) and "split_bf16"
+(PPOTrainer's default: the hidden layer on bf16 MFMAs, each fp32 operand split hi + lo).
 
 Tolerance: the kernel and hipBLASLt sum in different orders in fp32, so each gradient tensor
 must agree to rtol 1e-4 with atol 1e-6 x that tensor's largest magnitude (measured differences
