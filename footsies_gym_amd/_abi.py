@@ -6,7 +6,7 @@ the test-side oracle binding (``oracle/binding.py``) agree on layouts.
 """
 import ctypes as C
 
-FS_ABI_VERSION = 2
+FS_ABI_VERSION = 3
 
 FS_OK = 0
 FS_E_INVALID = -1
@@ -122,7 +122,7 @@ class fs_fighter_state(C.Structure):
         ("buffer_action_id", C.c_int32), ("reserve_action_id", C.c_int32),
         ("input_dir_history", C.c_uint32), ("attack_hold", C.c_int32),
         ("is_input_backward", C.c_uint8), ("is_reserve_proximity_guard", C.c_uint8),
-        ("has_won", C.c_uint8), ("pad0", C.c_uint8),
+        ("has_won", C.c_uint8), ("facing_flipped", C.c_uint8), ("position_y", C.c_float),
     ]
 
 

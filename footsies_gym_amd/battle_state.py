@@ -57,27 +57,27 @@ def _in_window(win, frame):
     return win[0] <= frame <= win[1]
 
 
-def _world_rect(rect, x, sign):
-    """TransformToFightRect (Fighter.cs:700-715), float32 arithmetic; position.y == 0."""
+def _world_rect(rect, x, y, sign):
+    """TransformToFightRect (Fighter.cs:700-715), float32 arithmetic."""
     f32 = np.float32
-    return {"x": float(f32(f32(x) + f32(f32(rect[0]) * f32(sign)))), "y": float(f32(rect[1])),
+    return {"x": float(f32(f32(x) + f32(f32(rect[0]) * f32(sign)))), "y": float(f32(f32(y) + f32(rect[1]))),
             "width": float(f32(rect[2])), "height": float(f32(rect[3]))}
 
 
-def _boxes(action_id, frame, x, face_right):
-    """ApplyCurrentActionData (Fighter.cs:671-697) for (action, frame) at position x."""
+def _boxes(action_id, frame, x, y, face_right):
+    """ApplyCurrentActionData (Fighter.cs:671-697) for (action, frame) at position (x, y)."""
     d = frame_data()
     a = d["by_id"][action_id]
     sign = 1 if face_right else -1
     base_hurt, base_push = d["fighter"]["base_hurtbox"], d["fighter"]["base_pushbox"]
-    hit = [{"rect": _world_rect(h["rect"], x, sign), "proximity": bool(h["proximity"]), "attackID": int(h["attack_id"])}
-           for h in a["hitboxes"] if _in_window(h["win"], frame)]
-    hurt = [_world_rect(base_hurt if h["use_base"] else h["rect"], x, sign)
+    hit = [{"rect": _world_rect(h["rect"], x, y, sign), "proximity": bool(h["proximity"]),
+            "attackID": int(h["attack_id"])} for h in a["hitboxes"] if _in_window(h["win"], frame)]
+    hurt = [_world_rect(base_hurt if h["use_base"] else h["rect"], x, y, sign)
             for h in a["hurtboxes"] if _in_window(h["win"], frame)]
     push = next((p for p in a["pushboxes"] if _in_window(p["win"], frame)), None)
     push_rect = base_push if push is None or push["use_base"] else push["rect"]
     velocity = next((m["velocity_x"] for m in a["movements"] if _in_window(m["win"], frame)), 0.0)
-    return hit, hurt, _world_rect(push_rect, x, sign), float(np.float32(velocity))
+    return hit, hurt, _world_rect(push_rect, x, y, sign), float(np.float32(velocity))
 
 
 def _input_arrays(dir_history, hold):
@@ -92,14 +92,16 @@ def _input_arrays(dir_history, hold):
     return [int(v) for v in inp[:-1]], [int(v) for v in down], [int(v) for v in up]
 
 
-def fighter_state(f, face_right):
+def fighter_state(f, is_p1):
     """One fs_fighter_state record -> FighterState dict (FighterState.cs field order)."""
     x = float(np.float32(f["position_x"]))
+    y = float(np.float32(f["position_y"]))
+    face_right = bool(is_p1) != bool(f["facing_flipped"])  # SetupBattleStart: isFaceRight = isPlayerOne
     act = int(f["action_id"])
-    hit, hurt, push, vel = _boxes(act, int(f["action_frame"]), x, face_right)
+    hit, hurt, push, vel = _boxes(act, int(f["action_frame"]), x, y, face_right)
     inp, down, up = _input_arrays(f["input_dir_history"], f["attack_hold"])
     return {
-        "position": [x, 0.0], "velocity_x": vel, "isFaceRight": bool(face_right),
+        "position": [x, y], "velocity_x": vel, "isFaceRight": face_right,
         "hitboxes": hit, "hurtboxes": hurt, "pushbox": push,
         "vitalHealth": int(f["vital"]), "guardHealth": int(f["guard"]),
         "currentActionID": act, "currentActionFrame": int(f["action_frame"]),
@@ -141,34 +143,26 @@ def dumps(state):
 
 
 class UnsupportedBattleStateError(FootsiesError, ValueError):
-    """A BattleState the simulator cannot continue exactly: Fighter.LoadState (Fighter.cs:741-744)
-    restores position.y and isFaceRight, but every state the game itself produces has y == 0 and
-    P1 facing right / P2 left (SetupBattleStart, Fighter.cs:120-135; nothing moves y or turns a
-    fighter).  A non-zero y would matter from the next tick on -- ApplyPositionChange(dx,
-    position.y) adds it on every push, and fighter2's mirrored push uses fighter1's y
-    (BattleCore.cs:492-498) -- and a flipped facing mirrors every box and input, so such a
-    state is refused rather than silently continued as a different game."""
+    """A BattleState the simulator cannot represent (a position that is not [x, y]).  Since round
+    4 position.y != 0 and a flipped isFaceRight are loaded as Fighter.LoadState restores them
+    (Fighter.cs:741-744) and run on the kernels' general-geometry tick (fs_set_state)."""
 
     def __init__(self, message):
         FootsiesError.__init__(self, _abi.FS_E_UNSUPPORTED, message)
 
 
 def _load_fighter(dst, s, is_p1):
-    """Fighter.LoadState (Fighter.cs:741-811) onto one fs_fighter_state record.  Raises
-    UnsupportedBattleStateError for a position.y other than 0 or a non-standard facing."""
+    """Fighter.LoadState (Fighter.cs:741-811) onto one fs_fighter_state record: position (x, y)
+    and isFaceRight as given (a y other than 0 or a facing other than the player's own runs on
+    the general-geometry tick, fs_set_state).  Raises UnsupportedBattleStateError for a position
+    that is not [x, y]."""
     who = "p1State" if is_p1 else "p2State"
     pos = list(s["position"])
     if len(pos) != 2:
         raise UnsupportedBattleStateError("%s.position must be [x, y], got %r" % (who, pos))
-    if np.float32(pos[1]) != 0:
-        raise UnsupportedBattleStateError(
-            "%s.position[1] = %r: the simulator keeps fighters on the ground (y = 0, as every state the game "
-            "produces); a non-zero y would shift every later push (BattleCore.cs:492-498)" % (who, pos[1]))
-    if bool(s["isFaceRight"]) != is_p1:
-        raise UnsupportedBattleStateError(
-            "%s.isFaceRight = %r: P1 always faces right and P2 left (Fighter.cs:124); a flipped fighter is "
-            "not supported" % (who, s["isFaceRight"]))
     dst["position_x"] = np.float32(pos[0])
+    dst["position_y"] = np.float32(pos[1])
+    dst["facing_flipped"] = int(bool(s["isFaceRight"]) != bool(is_p1))
     dst["action_id"] = int(s["currentActionID"])
     dst["action_frame"] = int(s["currentActionFrame"])
     dst["hit_count"] = int(s["currentActionHitCount"])

@@ -57,6 +57,8 @@ struct fs_context {
   uint4* delay_ring = nullptr;   // frame_delay > 0: [d][N] x 32-B observation records (fs_delay.hip)
   uint8_t* delay_head = nullptr; // frame_delay > 0: [N] each arena's ring head
   std::vector<uint8_t> p2bot;    // host mirror of each arena's P2 actor (1 = the bot)
+  bool geom = false;             // the last fs_set_state loaded a fighter with position.y != 0 or a flipped
+                                 // facing: steps run the kernels' general-geometry tick
   int p2bot_count = 0;
   std::vector<void*> allocations;
   uint64_t steps = 0;
@@ -209,7 +211,8 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
       (rc = dalloc(h, &h->st.aw, N)) || (rc = dalloc(h, &h->st.cum, N)))
     return fail(rc);
   // the game RNG and both BattleAIs exist in every mode (a P2 bot can be switched in later)
-  if ((rc = dalloc(h, &h->st.rng, N)) || (rc = dalloc(h, &h->st.bot, N)) || (rc = dalloc(h, &h->st.bot1, N)))
+  if ((rc = dalloc(h, &h->st.rng, N)) || (rc = dalloc(h, &h->st.bot, N)) || (rc = dalloc(h, &h->st.bot1, N)) ||
+      (rc = dalloc(h, &h->st.posy, N)))
     return fail(rc);
   h->p2bot.assign(N, cfg->p2_mode == FS_P2_BOT ? 1 : 0);
   h->p2bot_count = cfg->p2_mode == FS_P2_BOT ? h->n : 0;
@@ -318,6 +321,7 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
   sp.p1_bot = h->cfg.p1_mode == FS_P1_BOT;
   sp.p2_resets = h->cfg.p2_mode == FS_P2_BOT;
   sp.p2_noop = h->cfg.p2_mode == FS_P2_NOOP;
+  sp.geom = h->geom;
   if (pol) sp.pol = fsk::PolicyParams{pol->w1, pol->b1, pol->w2, pol->b2, pol->w3, pol->b3,
                                       pol->actions_out, pol->logp_out, pol->seed};
   const bool ext = h->cfg.p2_mode == FS_P2_EXTERNAL;
@@ -706,7 +710,7 @@ FS_API int fs_set_state(fs_handle h, const fs_arena_state* host_in) {
           f.hitstun > 31 || f.vital < 0 || f.vital > 3 || f.guard < 0 || f.guard > 3 || f.hit_count < 0 ||
           f.hit_count > 3 || f.attack_hold < 0 || f.attack_hold > 63 ||
           (f.buffer_action_id != -1 && !valid_action_id(f.buffer_action_id)) ||
-          (f.reserve_action_id != -1 && !valid_action_id(f.reserve_action_id)))
+          (f.reserve_action_id != -1 && !valid_action_id(f.reserve_action_id)) || f.facing_flipped > 1)
         return set_err(h, FS_E_INVALID, "fs_set_state: arena %d fighter %d out of representable range", i, k);
     }
     if (s.recording_count < 0 || s.recording_count > 18000)
@@ -732,6 +736,12 @@ FS_API int fs_set_state(fs_handle h, const fs_arena_state* host_in) {
   (void)hipFree(d);
   if (e != hipSuccess) return set_err(h, FS_E_DEVICE, "fs_set_state: %s", hipGetErrorString(e));
   for (int i = 0; i < h->n; i++) set_p2bot_mirror(h, (size_t)i, host_in[i].p2_bot);
+  // every arena was replaced: the general-geometry tick is needed iff a loaded fighter is off the
+  // ground or faces the other way (-0.0 counts as 0: it moves no box and doubles to itself)
+  bool geom = false;
+  for (int i = 0; i < h->n && !geom; i++)
+    for (int k = 0; k < 2; k++) geom = geom || host_in[i].f[k].position_y != 0.0f || host_in[i].f[k].facing_flipped;
+  h->geom = geom;
   return FS_OK;
 }
 
@@ -761,7 +771,7 @@ FS_API int fs_set_stream(fs_handle h, void* stream) {
 FS_API const char* fs_step_kernel(fs_handle h, int n_steps, int flags) {
   if (!h || n_steps <= 0 || (flags & ~(FS_KERNEL_HASHED | FS_KERNEL_POLICY))) return nullptr;
   return fsk::step_kernel_name((flags & FS_KERNEL_POLICY) != 0, (flags & FS_KERNEL_HASHED) != 0, n_steps, h->n,
-                               h->cfg.float_mode, variant(h));
+                               h->cfg.float_mode, variant(h), h->geom);
 }
 
 FS_API int fs_num_envs(fs_handle h) { return h ? h->n : 0; }

@@ -32,6 +32,7 @@ struct DevState {
   uint4* rng;      // the game's UnityEngine.Random Xorshift128 state (every mode)
   uint2* bot;      // P2's BattleAI: (bot word, previous FightState distance bits), layout in fs_kernels.hip
   uint2* bot1;     // P1's BattleAI (FS_P1_BOT), same layout
+  float2* posy;    // y of P1, P2 (Fighter.position.y): 0 unless a state load set it (general geometry)
 };
 
 // The kernels' P2 variants.  FS_P2_EXTERNAL / FS_P2_BOT / FS_P2_NOOP run handles whose actors are
@@ -86,6 +87,7 @@ struct StepParams {
   int p2_resets;  // kActors: P2's bot is Reset at Intro (the handle was created with FS_P2_BOT)
   int p2_noop;    // kActors: a non-bot P2 presses nothing (FS_P2_NOOP handle)
   int prio;       // fused launches: time-sliced wave priority (set by the launcher, prio_slice)
+  int geom;       // some arena has position.y != 0 or a flipped facing: the general-geometry tick
   // host actions of a one-tick launch over at most kInlineArenas arenas, carried in the kernel
   // arguments instead of a staging copy (inl_n != 0): byte a of inl[player] is arena a's input
   int inl_n;
@@ -126,7 +128,8 @@ struct DelayParams {
 // launchers (fs_kernels.hip, fs_delay.hip); return hipError_t of the launch
 // variant: FS_P2_EXTERNAL / FS_P2_BOT / FS_P2_NOOP or kActors (see above)
 hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStream_t s);
-const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant);
+const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant,
+                             bool geom);
 hipError_t launch_reset(const ResetParams& p, int float_mode, hipStream_t s);
 hipError_t launch_set_p2(const DevState& st, int bot, const uint8_t* mask, int n, hipStream_t s);
 hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint64_t arena_base, uint8_t* p1,

@@ -71,7 +71,8 @@ constexpr int kTabLds = 0, kTabGlobal = 1;
 // packed fighter word (u64), one per fighter in DevState::fpk
 //   [0,5) action idx | [5,14) action frame | [14,19) hitstun | [19,21) vital |
 //   [21,23) guard | [23,25) hit count | [25,30) buffer idx | [30,35) reserve idx |
-//   35 isInputBackward | 36 isReserveProximityGuard | 37 hasWon | [38,44) attack hold
+//   35 isInputBackward | 36 isReserveProximityGuard | 37 hasWon | [38,44) attack hold |
+//   44 facing flipped (isFaceRight != isPlayerOne, only after a state load)
 // arena header word (DevState::aw.y)
 //   [0,15) recording count | [15,18) rec P1 | [18,21) rec P2 | [21,24) remote actor P1 input |
 //   [24,27) remote actor P2 input | 27 reset pending | 28 has_terminated | 29 P2's actor is the bot
@@ -92,10 +93,14 @@ struct Fighter {
   int act, frame, stun, vital, guard, hits, buf, rsv, hold;
   uint32_t in_back, prox, won;  // flags as 0 / 1 words (a carried bool is re-masked at every test)
   // boxes of this tick (UpdateBoxes, F:671-697): the frame record holds their geometry,
-  // the fighter their world x (y == rect.y since position.y is always 0)
+  // the fighter their world x (y == rect.y while position.y is 0)
   int rec;        // frame record index of (action, frame)
   float px, ux0, ux1, hx0, hx1;  // world x: pushbox, hurtbox 0 / 1, hitbox 0 / 1
   float pw, phw;  // pushbox width of the record, and width / 2
+  // General geometry (a launch with StepParams::geom; otherwise flip == 0 and y == 0 throughout):
+  uint32_t flip;  // isFaceRight != isPlayerOne (LoadState F:744; SetupBattleStart F:124 clears it)
+  float y;        // position.y
+  float py, uy0, uy1, hy0, hy1;  // world y (rect.y) of the pushbox, hurtboxes 0 / 1, hitboxes 0 / 1
 };
 
 struct Arena {
@@ -123,13 +128,14 @@ __device__ __forceinline__ void unpack_fighter(Fighter& f, uint32_t lo, uint32_t
   f.prox = (w >> 36) & 1;
   f.won = (w >> 37) & 1;
   f.hold = (int)((w >> 38) & 63);
+  f.flip = (w >> 44) & 1;
 }
 
 __device__ __forceinline__ uint64_t pack_fighter(const Fighter& f) {
   return (uint64_t)f.act | ((uint64_t)f.frame << 5) | ((uint64_t)f.stun << 14) | ((uint64_t)f.vital << 19) |
          ((uint64_t)f.guard << 21) | ((uint64_t)f.hits << 23) | ((uint64_t)f.buf << 25) |
          ((uint64_t)f.rsv << 30) | ((uint64_t)f.in_back << 35) | ((uint64_t)f.prox << 36) |
-         ((uint64_t)f.won << 37) | ((uint64_t)f.hold << 38);
+         ((uint64_t)f.won << 37) | ((uint64_t)f.hold << 38) | ((uint64_t)f.flip << 44);
 }
 
 __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
@@ -142,6 +148,9 @@ __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
   unpack_fighter(A.f1, pk.z, pk.w);
   A.f0.x = pos.x;
   A.f1.x = pos.y;
+  const float2 py = s.posy[i];
+  A.f0.y = py.x;
+  A.f1.y = py.y;
   A.f0.hist = hist.x;  // split form (get/set convert)
   A.f1.hist = hist.y;
   A.frame_count = aw.x;
@@ -162,6 +171,7 @@ __device__ __forceinline__ void load_arena(Arena& A, const DevState& s, int i) {
 __device__ __forceinline__ void store_arena(const Arena& A, const DevState& s, int i) {
   uint64_t w0 = pack_fighter(A.f0), w1 = pack_fighter(A.f1);
   s.pos[i] = make_float2(A.f0.x, A.f1.x);
+  s.posy[i] = make_float2(A.f0.y, A.f1.y);
   s.hist[i] = make_uint2(A.f0.hist, A.f1.hist);
   s.fpk[i] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   uint32_t h = A.rec_count | (A.rec1 << 15) | (A.rec2 << 18) | (A.act1 << 21) | (A.act2 << 24) |
@@ -440,10 +450,42 @@ __device__ __forceinline__ void apply_position_change(Fighter& f, float dx) {
   f.hx1 = hx.y;
 }
 
+// General geometry (StepParams::geom: some fighter was loaded with position.y != 0 or a flipped
+// facing).  The box y extents come from kRecY (fs_tables.h) instead of ybits / the constant
+// pushbox y-test, the world y of every box is position.y + rect.y (TransformToFightRect
+// F:706-719), and the pushes carry position.y through ApplyPositionChange as the C# does: both
+// UpdatePushCharacterVs* calls pass a fighter's position.y as the y shift (BC:491-498, 511-515),
+// so every push adds y to itself (P2's shift in the P1-right-of-P2 case is P1's y after P1's own
+// shift).  A fighter whose y is 0 gets the same results as on the standard path.
+struct RecY {
+  F4 a, b, c;  // {push y, h, hurt 0 y, h}, {hurt 1 y, h, hit 0 y, h}, {hit 1 y, h, -, -}
+};
+__device__ __forceinline__ RecY rec_y(uint32_t rec) {
+  const F4* t = reinterpret_cast<const F4*>(kRecY);
+  return RecY{t[3 * rec], t[3 * rec + 1], t[3 * rec + 2]};
+}
+template <int FM>
+__device__ __forceinline__ void update_boxes_y(Fighter& f, const RecY& Y) {
+  f.py = fadd<FM>(f.y, Y.a.x);
+  f.uy0 = fadd<FM>(f.y, Y.a.z);
+  f.uy1 = fadd<FM>(f.y, Y.b.x);
+  f.hy0 = fadd<FM>(f.y, Y.b.z);
+  f.hy1 = fadd<FM>(f.y, Y.c.x);
+}
+template <int FM>
+__device__ __forceinline__ void apply_position_change_y(Fighter& f, float dy) {  // F:334-349, the y half
+  f.y = fadd<FM>(f.y, dy);
+  f.py = fadd<FM>(f.py, dy);
+  f.uy0 = fadd<FM>(f.uy0, dy);
+  f.uy1 = fadd<FM>(f.uy1, dy);
+  f.hy0 = fadd<FM>(f.hy0, dy);
+  f.hy1 = fadd<FM>(f.hy1, dy);
+}
+
 // UpdatePushCharacterVsBackground (BC:503-519) with BoxBase semantics
 // Branch-free: with no push the shift is -0.0, the exact identity of IEEE addition (x + -0.0 == x
 // bit for bit, -0.0 included), so every lane applies it.
-template <int FM>
+template <int FM, bool GEOM = false>
 __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
   // BoxBase xMin / xMax (F:12-13) with the record's exact width / 2 (w / 2 is exact in binary32,
   // and (double)(w / 2) == (double)w / 2 for the binary64 model)
@@ -453,6 +495,10 @@ __device__ __forceinline__ void push_character_vs_background(Fighter& f) {
   asm volatile("" : "+v"(d_lo), "+v"(d_hi));  // both computed: selects, not a branch
   const float dx = xmin < -kStageHalf ? d_lo : (xmax > kStageHalf ? d_hi : -0.0f);
   apply_position_change<FM>(f, dx);
+  if constexpr (GEOM) {  // ApplyPositionChange(dx, f.position.y) on a push; x + -0.0 == x otherwise
+    const bool pushed = (xmin < -kStageHalf) | (xmax > kStageHalf);
+    apply_position_change_y<FM>(f, pushed ? f.y : -0.0f);
+  }
 }
 
 // BoxBase (F:8-26): boxes are (world x, width/2, yMin, yMax); xMin = x - w/2, xMax = x + w/2
@@ -954,13 +1000,20 @@ __device__ __forceinline__ void store_lane(const Lane& L, const DevState& s, int
 // shift.  The y-test is constant: tools/gen_tables.py proves every pair of pushboxes
 // overlaps vertically (kPushYAlwaysOverlaps) and keeps no y extents in the records.
 static_assert(kPushYAlwaysOverlaps, "the frame records keep no pushbox y extents");
-template <int FM>
-__device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t k) {
+template <int FM, bool GEOM = false>
+__device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t k, float ph = 0.0f) {
   // The test and the shift are symmetric in the two fighters, so each lane evaluates them
   // as (mine, partner's) -- the same operations on the same values as (P1, P2).
   const float o_px = xpair(f.px), o_x = xpair(f.x), o_pw = xpair(f.pw);
   const float xmax_m = fadd<FM>(f.pw, f.px), xmax_o = fadd<FM>(o_pw, o_px);  // Rect.xMax = width + x
-  const bool overlap = (xmax_o > f.px) & (o_px < xmax_m);
+  bool overlap = (xmax_o > f.px) & (o_px < xmax_m);
+  float o_y = 0.0f;
+  if constexpr (GEOM) {  // the y half of Rect.Overlaps (yMax = height + y), ph = my pushbox height
+    const float o_py = xpair(f.py), o_ph = xpair(ph);
+    o_y = xpair(f.y);
+    const float ymax_m = fadd<FM>(ph, f.py), ymax_o = fadd<FM>(o_ph, o_py);
+    overlap = overlap & (ymax_o > f.py) & (o_py < ymax_m);
+  }
   if (!overlap || f.x == o_x) return;  // a tie pushes nothing (BC:490-499)
   const bool left = f.x < o_x;         // the left fighter moves by -d/2, the right one by +d/2
   float dx;
@@ -972,6 +1025,8 @@ __device__ __forceinline__ void push_character_vs_character(Fighter& f, uint32_t
     dx = left ? d * -1.0f / 2.0f : d * 1.0f / 2.0f;
   }
   apply_position_change<FM>(f, dx);
+  // P1 shifts by its own y; P2 by its own when P1 is on the left, else by P1's y after P1's shift
+  if constexpr (GEOM) apply_position_change_y<FM>(f, (k == 1 && o_x > f.x) ? fadd<FM>(o_y, o_y) : f.y);
 }
 
 // UpdateHitboxHurtboxCollision (BC:521-591): attacker P1 (phase A), then attacker P2
@@ -1084,6 +1139,8 @@ __device__ __forceinline__ void end_tick(Fighter& f, bool won) {
 // SetupBattleStart (F:120-135): hitstun and the two guard latches are NOT reset
 __device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {
   f.x = x;
+  f.y = 0.0f;   // position = startPosition (x, 0) (BC:264-265)
+  f.flip = 0;   // isFaceRight = isPlayerOne (F:124)
   f.vital = 1;
   f.guard = kStartGuard;
   f.won = false;
@@ -1321,7 +1378,7 @@ __device__ __forceinline__ void opaque_burst_results(Lane& L) {
                "+v"(L.rec_count));
 }
 
-template <int FM, int P2, int WAIT = -1, int TP = kTabLds>
+template <int FM, int P2, int WAIT = -1, int TP = kTabLds, bool GEOM = false>
 __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   constexpr bool G = TP == kTabGlobal;  // the tables from global memory: a one-tick launch (k_step),
@@ -1363,7 +1420,9 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.rec = in;
     L.rec_count++;
   }
-  const InputEval e = update_input(L.f, in, k ? kRelLut1 : kRelLut0);
+  // the fighter's facing: the player's own, or flipped by a state load (general geometry)
+  const uint32_t face = GEOM ? k ^ L.f.flip : k;
+  const InputEval e = update_input(L.f, in, face ? kRelLut1 : kRelLut0);
   const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
   increment_action_frame(L.f, ai);
   // the record if the action continues, read alongside the request entry; a
@@ -1376,7 +1435,7 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   // record, the y half of the box-pair overlaps (records only, kTables.ybits) and the hit
   // resolution of the partner's record at its hit count (the record index and the hit count
   // cross the pair first).
-  const RecGeo R = frame_rec<G>(k, (uint32_t)L.f.rec);
+  const RecGeo R = frame_rec<G>(face, (uint32_t)L.f.rec);
   const uint32_t o_rec = (uint32_t)xpair(L.f.rec);
   const uint32_t o_hits = (uint32_t)xpair(L.f.hits);
   static_assert(kNumFrameRecs <= 64, "ybits rows are 64 records wide");
@@ -1384,16 +1443,30 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   const U4 res = reinterpret_cast<const U4*>(tabs<G>().resolve)[__umul24(o_hits, (uint32_t)kNumFrameRecs) + o_rec];
   update_movement<FM>(L.f, R.push.z);
   update_boxes<FM>(L.f, R);
+  RecY Y;
+  if constexpr (GEOM) {
+    Y = rec_y((uint32_t)L.f.rec);
+    update_boxes_y<FM>(L.f, Y);
+  }
   // the partner's hitbox half-widths (its own record's)
   const float o_hw0 = xpair(R.hit.z), o_hw1 = xpair(R.hit.w);
-  push_character_vs_character<FM>(L.f, k);
-  push_character_vs_background<FM>(L.f);
+  push_character_vs_character<FM, GEOM>(L.f, k, GEOM ? Y.a.y : 0.0f);
+  push_character_vs_background<FM, GEOM>(L.f);
   // consumed here, unconditionally, so the reads stay where they were issued (next to the
   // frame record) instead of being sunk into the collision's branch
   // (R.push too: a register of a load in flight that the allocator considers free is reused at
   // once, which forces a wait for the load)
   asm volatile("" ::"v"(R.push), "v"(R.hurt), "v"(o_hw0), "v"(o_hw1), "v"(res), "v"(ym));
-  hitbox_hurtbox_collision<FM>(L.f, k, R.hurt, o_hw0, o_hw1, res, ym);
+  uint32_t ym_t = ym;
+  if constexpr (GEOM) {  // the y half of BoxBase.Overlaps (F:17-25) from the boxes' y after the pushes
+    const float o_hy0 = xpair(L.f.hy0), o_hy1 = xpair(L.f.hy1), o_hh0 = xpair(Y.b.w), o_hh1 = xpair(Y.c.y);
+    const float hymax0 = fadd<FM>(o_hy0, o_hh0), hymax1 = fadd<FM>(o_hy1, o_hh1);  // partner's hitboxes
+    const float uymax0 = fadd<FM>(L.f.uy0, Y.a.w), uymax1 = fadd<FM>(L.f.uy1, Y.b.y);  // my hurtboxes
+    auto ov = [](float uy, float uymax, float hy, float hymax) { return (uint32_t)((uymax >= hy) & (uy <= hymax)); };
+    ym_t = ov(L.f.uy0, uymax0, o_hy0, hymax0) | (ov(L.f.uy1, uymax1, o_hy0, hymax0) << 1) |
+           (ov(L.f.uy0, uymax0, o_hy1, hymax1) << 2) | (ov(L.f.uy1, uymax1, o_hy1, hymax1) << 3);
+  }
+  hitbox_hurtbox_collision<FM>(L.f, k, R.hurt, o_hw0, o_hw1, res, ym_t);
   // the next tick's ActionInfo, issued now so its LDS latency hides behind the KO test, the
   // reward and the stores (only the same-step reset below changes the action again: to STAND)
   if constexpr (!G) L.ai = action_info<G>(L.f.act);
@@ -1471,7 +1544,7 @@ __device__ __forceinline__ void policy_features(const Lane& L, uint32_t& d0, uin
 // POL samples P1's action every tick from the MLP actor (fs_policy.h); its MFMAs and lane
 // exchanges need the whole wave, so lanes past the last arena stay in the loop (on a copy
 // of arena 0 that they never store) unless their whole wave is idle.
-template <int FM, int P2, bool FUSED, bool HASH, bool POL = false>
+template <int FM, int P2, bool FUSED, bool HASH, bool POL = false, bool GEOM = false>
 __device__ __forceinline__ void step_body(const StepParams& p) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = l < 2 * p.n_envs;
@@ -1497,6 +1570,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
   // the arena state and the first action are in flight while the block stages the tables
   Lane L;
   load_lane<P2>(L, p.st, a, k);
+  if constexpr (GEOM) L.f.y = reinterpret_cast<const float*>(p.st.posy)[2 * a + (int)k];
   // the fused loop's rows: every lane loads (so the in-flight register is written by the load
   // alone); a lane without a row of its own reads P1's row 0, always valid in these launches,
   // and ignores it.  Rows 0 and 1 are both in flight while the block stages the tables.
@@ -1537,7 +1611,8 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
           if (p.pol.actions) p.pol.actions[row] = (uint8_t)po.action;
           if (p.pol.logp) p.pol.logp[row] = po.logp;
         }
-        env_step<FM, P2>(L, k == 0 ? po.action : act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
+        env_step<FM, P2, -1, kTabLds, GEOM>(L, k == 0 ? po.action : act & 7u, p, (uint32_t)t * row_step + (uint32_t)a,
+                                            next);
       }
       policy_features(L, d0, d1);
     }
@@ -1549,7 +1624,7 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
         const uint32_t act = next;
         next = fetch(min(t + 1, p.n_steps - 1));
         if (p.prio) prio_slice(grp);
-        env_step<FM, P2>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
+        env_step<FM, P2, -1, kTabLds, GEOM>(L, act & 7u, p, (uint32_t)t * row_step + (uint32_t)a, next);
       }
     } else {
       // Rows two ticks ahead, loaded and waited for as described at row_load, in two registers
@@ -1566,22 +1641,27 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       for (; t < last; t += 2) {
         a_fl = issue(t + 2);
         if (p.prio) prio_slice(grp);
-        env_step<FM, P2, 11>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
+        env_step<FM, P2, 11, kTabLds, GEOM>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
         b_rd = b_fl;
         b_fl = issue(t + 3);
         if (p.prio) prio_slice(grp);
-        env_step<FM, P2, 11>(L, reads ? b_rd & 7u : 0u, p, (uint32_t)(t + 1) * row_step + (uint32_t)a, a_fl);
+        env_step<FM, P2, 11, kTabLds, GEOM>(L, reads ? b_rd & 7u : 0u, p, (uint32_t)(t + 1) * row_step + (uint32_t)a,
+                                            a_fl);
         a_rd = a_fl;
       }
       if (t == last) {  // an odd tick count: the last tick waits for a re-read of the last row
         a_fl = issue(t + 2);
         uint32_t b_last = b_fl;  // (b_fl itself stays the in-flight value for the final wait)
-        env_step<FM, P2, 11>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_last);
+        env_step<FM, P2, 11, kTabLds, GEOM>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a,
+                                            b_last);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::"v"(a_fl), "v"(b_fl) : "memory");  // no load outlives the wave
     }
   }
-  if (active) store_lane<P2>(L, p.st, a);
+  if (active) {
+    store_lane<P2>(L, p.st, a);
+    if constexpr (GEOM) reinterpret_cast<float*>(p.st.posy)[2 * a + (int)k] = L.f.y;
+  }
 }
 
 // The one-tick launch (fs_step, fs_step_masked: the VectorEnv.step path).  Nothing is amortized
@@ -1610,8 +1690,9 @@ __device__ __forceinline__ void step_one(const StepParams& p) {
   const int n_envs = p.n_envs, inl_n = p.inl_n;
   // (inputs only: the pointers keep their global-memory provenance; and the two row pointers each
   // have a use of their own here, so `k ? q2 : q1` stays a register select)
+  const int geom = p.geom;
   asm volatile("" ::"s"(p.st.pos), "s"(p.st.hist), "s"(p.st.fpk), "s"(p.st.aw), "s"(p.st.cum), "s"(q1), "s"(q2),
-               "s"(qm), "s"(n_envs), "s"(inl_n));
+               "s"(qm), "s"(n_envs), "s"(inl_n), "s"(geom));
   const int l = blockIdx.x * kBlock + threadIdx.x;
   const bool active = l < 2 * n_envs;
   const int a = active ? l >> 1 : 0;
@@ -1639,8 +1720,16 @@ __device__ __forceinline__ void step_one(const StepParams& p) {
   L.ai.z = L.ai.w = 0u;  // (the cancel mask and padding: not read by the tick)
   if (!active || !on) return;
   uint32_t none = 0;
-  env_step<FM, P2, -1, kTabGlobal>(L, in & 7u, p, (uint32_t)a, none);
-  store_lane<P2>(L, p.st, a);
+  if (geom) {  // (general geometry: position.y, read after the branch; off the common path)
+    float* py = reinterpret_cast<float*>(p.st.posy) + 2 * a + (int)k;
+    L.f.y = *py;
+    env_step<FM, P2, -1, kTabGlobal, true>(L, in & 7u, p, (uint32_t)a, none);
+    store_lane<P2>(L, p.st, a);
+    *py = L.f.y;
+  } else {
+    env_step<FM, P2, -1, kTabGlobal>(L, in & 7u, p, (uint32_t)a, none);
+    store_lane<P2>(L, p.st, a);
+  }
 }
 
 template <int FM, int P2>
@@ -1648,19 +1737,24 @@ __global__ __launch_bounds__(256) void k_step(StepParams p) {
   step_one<FM, P2>(p);
 }
 
+// Each fused kernel holds the standard tick and the general-geometry one (StepParams::geom,
+// uniform over the launch) as two loops: the standard loop carries none of the y state.
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n(StepParams p) {
-  step_body<FM, P2, true, false>(p);
+  if (p.geom) step_body<FM, P2, true, false, false, true>(p);
+  else step_body<FM, P2, true, false>(p);
 }
 
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n_hashed(StepParams p) {
-  step_body<FM, P2, true, true>(p);
+  if (p.geom) step_body<FM, P2, true, true, false, true>(p);
+  else step_body<FM, P2, true, true>(p);
 }
 
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n_policy(StepParams p) {
-  step_body<FM, P2, true, false, true>(p);
+  if (p.geom) step_body<FM, P2, true, false, true, true>(p);
+  else step_body<FM, P2, true, false, true>(p);
 }
 
 // FootsiesEnv.reset (FE:482-515) / RESET (BC:143-146) / game start (BC:105-128), every handle
@@ -1683,6 +1777,8 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
     L.f.frame = L.f.stun = L.f.vital = L.f.guard = L.f.hits = L.f.hold = 0;
     L.f.buf = L.f.rsv = NONE;
     L.f.in_back = L.f.prox = L.f.won = false;
+    L.f.flip = 0;
+    L.f.y = 0.0f;
     L.frame_count = 0;
     L.rec_count = L.rec = L.act = L.bin = 0;
     L.pending = false;
@@ -1695,10 +1791,12 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
     L.fb.ready = false;
   } else {
     load_lane<kActors>(L, p.st, a, k);
+    L.f.y = reinterpret_cast<const float*>(p.st.posy)[l];
   }
   if (p.seeds) L.rng = rng_init((int32_t)(uint32_t)p.seeds[a]);  // SEED (BC:170-173)
   if (p.flags == FS_RESET_SEED_ONLY) {
     store_lane<kActors>(L, p.st, a);
+    reinterpret_cast<float*>(p.st.posy)[l] = L.f.y;
     return;
   }
   const bool hard = p.init || p.flags == FS_RESET_HARD || !L.has_term;
@@ -1716,6 +1814,7 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
     p.out.truncated[a] = 0;
   }
   store_lane<kActors>(L, p.st, a);
+  reinterpret_cast<float*>(p.st.posy)[l] = L.f.y;
 }
 
 // P2_BOT (BC:158-167): P2's actor of the masked arenas becomes the bot (bot = 1) or the remote actor
@@ -1779,12 +1878,13 @@ __global__ __launch_bounds__(256) void k_get_state(DevState st, fs_arena_state* 
       g.guard = f.guard;
       g.buffer_action_id = f.buf == NONE ? -1 : kActionId[f.buf];
       g.reserve_action_id = f.rsv == NONE ? -1 : kActionId[f.rsv];
-      g.input_dir_history = raw_hist(f.hist, k);
+      g.input_dir_history = raw_hist(f.hist, k ^ (int)f.flip);  // (the history is kept facing-relative)
       g.attack_hold = f.hold;
       g.is_input_backward = f.in_back;
       g.is_reserve_proximity_guard = f.prox;
       g.has_won = f.won;
-      g.pad0 = 0;
+      g.facing_flipped = (uint8_t)f.flip;
+      g.position_y = f.y;
     }
     s.frame_count = A.frame_count;
     s.recording_count = (int32_t)A.rec_count;
@@ -1870,6 +1970,8 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
     const fs_fighter_state& g = s.f[k];
     Fighter& f = k == 0 ? A.f0 : A.f1;
     f.x = g.position_x;
+    f.y = g.position_y;
+    f.flip = g.facing_flipped & 1u;
     f.act = action_index_of(g.action_id);
     f.frame = g.action_frame;
     f.hits = g.hit_count;
@@ -1878,7 +1980,7 @@ __global__ __launch_bounds__(256) void k_set_state(DevState st, const fs_arena_s
     f.guard = g.guard;
     f.buf = g.buffer_action_id < 0 ? NONE : action_index_of(g.buffer_action_id);
     f.rsv = g.reserve_action_id < 0 ? NONE : action_index_of(g.reserve_action_id);
-    f.hist = split_hist(g.input_dir_history, k);
+    f.hist = split_hist(g.input_dir_history, k ^ (int)f.flip);
     f.hold = g.attack_hold;
     f.in_back = g.is_input_backward;
     f.prox = g.is_reserve_proximity_guard;
@@ -1955,7 +2057,8 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   else if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
   else if constexpr (P2 != kActors) {
-    if (fused_one_lane(p.n_envs)) hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
+    // (the one-lane kernel has no general-geometry tick: a geom launch takes the two-lane one)
+    if (!p.geom && fused_one_lane(p.n_envs)) hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
     else hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
   } else {
     hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
@@ -1979,10 +2082,10 @@ hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStre
 }
 
 // The kernel launch_step_p2 runs for a launch of this shape, as rocprofv3 names it (fs_step_kernel).
-const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant) {
+const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant, bool geom) {
   static thread_local char buf[64];
   const char* k = policy ? "k_step_n_policy" : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step"
-                : (variant != kActors && fused_one_lane(n_envs)) ? "k_step_n1" : "k_step_n";
+                : (variant != kActors && !geom && fused_one_lane(n_envs)) ? "k_step_n1" : "k_step_n";
   snprintf(buf, sizeof buf, "fsk::%s<%d, %d>", k, float_mode == FS_FLOAT_DOUBLE ? 1 : 0, variant);
   return buf;
 }

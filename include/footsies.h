@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 2
+#define FS_ABI_VERSION 3
 
 /* error codes */
 #define FS_OK 0
@@ -156,7 +156,12 @@ typedef struct fs_fighter_state {
   uint8_t is_input_backward;
   uint8_t is_reserve_proximity_guard;
   uint8_t has_won;
-  uint8_t pad0;
+  uint8_t facing_flipped;       /* 0: the player's own facing (P1 right, P2 left: SetupBattleStart, F:124);
+                                   1: the other (Fighter.isFaceRight restored by LoadState, F:744) */
+  float position_y;             /* Fighter.position.y (F:742): 0 in every state the game reaches by itself;
+                                   a loaded y moves every box (TransformToFightRect F:706-719) and is added
+                                   to itself by every push (BC:483-519 pass position.y to
+                                   ApplyPositionChange, F:331-350) until the next round start (F:123) */
 } fs_fighter_state;
 
 typedef struct fs_arena_state {
@@ -368,7 +373,10 @@ int fs_bind_outputs(fs_handle h, const fs_outputs* dev);
 int fs_get_env_state(fs_handle h, fs_env_state* host_out);
 int fs_get_state(fs_handle h, fs_arena_state* host_out);
 /* Load canonical state [N] from host (STATE_LOAD, BC:153-156, 676-683).
- * Input history beyond what fs_arena_state carries is not representable.
+ * Input history beyond what fs_arena_state carries is not representable.  Fighters with
+ * position_y != 0 or facing_flipped switch the handle's steps to the kernels' general-geometry
+ * path (box y extents tested, y carried through the pushes) until the next fs_set_state loads
+ * only standard fighters.
  * FS_E_INVALID (nothing loaded) for a field outside the packed layout's range, or, with the
  * bot as P2, a queue index at or past its plan's length (such a queue is empty: plan -1). */
 int fs_set_state(fs_handle h, const fs_arena_state* host_in);

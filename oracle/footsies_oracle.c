@@ -1335,6 +1335,8 @@ OR_EXPORT int or_get_state(or_handle C, fs_arena_state* out) {
       g->is_input_backward = (uint8_t)f->is_input_backward;
       g->is_reserve_proximity_guard = (uint8_t)f->is_reserve_proximity_guard;
       g->has_won = (uint8_t)f->has_won;
+      g->facing_flipped = (uint8_t)(f->is_face_right != (k == 0)); /* SetupBattleStart: isFaceRight = isPlayerOne */
+      g->position_y = f->pos_y;
     }
     s->frame_count = A->frame_count;
     s->recording_count = (int32_t)A->rec_idx;
@@ -1406,8 +1408,9 @@ OR_EXPORT int or_set_state(or_handle C, const fs_arena_state* in) {
     for (int k = 0; k < 2; k++) {
       fighter_t* f = &A->f[k];
       const fs_fighter_state* g = &s->f[k];
-      f->pos_x = g->position_x;
-      f->pos_y = 0.0f;
+      f->pos_x = g->position_x; /* LoadState (F:741-744) */
+      f->pos_y = g->position_y;
+      f->is_face_right = (k == 0) != (g->facing_flipped != 0);
       f->action_id = g->action_id;
       f->action_frame = g->action_frame;
       f->hit_count = g->hit_count;

@@ -42,7 +42,8 @@ static bool same_fighter(const fs_fighter_state& a, const fs_fighter_state& b) {
          a.vital == b.vital && a.guard == b.guard && a.buffer_action_id == b.buffer_action_id &&
          a.reserve_action_id == b.reserve_action_id && a.input_dir_history == b.input_dir_history &&
          a.attack_hold == b.attack_hold && a.is_input_backward == b.is_input_backward &&
-         a.is_reserve_proximity_guard == b.is_reserve_proximity_guard && a.has_won == b.has_won;
+         a.is_reserve_proximity_guard == b.is_reserve_proximity_guard && a.has_won == b.has_won &&
+         a.facing_flipped == b.facing_flipped && memcmp(&a.position_y, &b.position_y, 4) == 0;
 }
 static bool same_arena(const fs_arena_state& a, const fs_arena_state& b, bool bot) {
   bool ok = same_fighter(a.f[0], b.f[0]) && same_fighter(a.f[1], b.f[1]) && a.frame_count == b.frame_count &&

@@ -67,13 +67,15 @@ def random_bot_fields(n, rng, prefix=""):
             prefix + "prev_opponent_action": rng.choice(ids, n)}
 
 
-def random_states(n, rng, p2="external", p2_bot_frac=0.0):
+def random_states(n, rng, p2="external", p2_bot_frac=0.0, geom_frac=0.0):
     """Arbitrary loadable arena states (fs_arena_state), not only ones reachable from a reset:
     any action at any frame up to its frameCount, buffered / reserved actions, hitstun, latches,
     hasWon, saturated recordings, random histories and bot queues -- the paths a played match
     reaches rarely (the hasWon request, reserve / buffer takes, DEAD past frame 63).  The actors
     fit the handle's P2 mode: a bot-created P2 is the bot and ready; with a remote P2 a fraction
-    `p2_bot_frac` of the arenas has the bot switched in (bot_ready random: a never-Reset bot)."""
+    `p2_bot_frac` of the arenas has the bot switched in (bot_ready random: a never-Reset bot).
+    `geom_frac` of the fighters are loaded off the ground (position.y in +-1.5, some exact box
+    edges) and, independently, with a flipped facing (the general-geometry tick)."""
     st = np.zeros(n, dtype=np.ctypeslib.as_array((_abi.fs_arena_state * 1)()).dtype)
     ids = np.array(sorted(ACTION_FRAMES), dtype=np.int32)
     for k in range(2):
@@ -93,6 +95,11 @@ def random_states(n, rng, p2="external", p2_bot_frac=0.0):
         f["is_input_backward"] = rng.integers(0, 2, n)
         f["is_reserve_proximity_guard"] = rng.integers(0, 2, n)
         f["has_won"] = (rng.random(n) < 0.1).astype(np.uint8)
+        if geom_frac:
+            y = rng.choice(np.array([0.25, -0.25, 0.5, 1.0, -1.2, 0.1], np.float32), n)
+            y = np.where(rng.random(n) < 0.5, y, rng.uniform(-1.5, 1.5, n).astype(np.float32))
+            f["position_y"] = np.where(rng.random(n) < geom_frac, y, np.float32(0.0)).astype(np.float32)
+            f["facing_flipped"] = (rng.random(n) < geom_frac).astype(np.uint8)
     st["frame_count"] = rng.integers(0, 5000, n)
     st["recording_count"] = np.where(rng.random(n) < 0.2, 18000, rng.integers(0, 18000, n))
     st["recording_last"] = rng.integers(0, 8, (n, 2))

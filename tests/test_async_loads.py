@@ -22,9 +22,9 @@ def test_wait_counts_are_proven_and_a_too_deep_wait_is_caught(tmp_path):
     waits claim 30 (more than the stores of one tick plus a load) must be reported."""
     src = os.path.join(ROOT, "footsies_gym_amd", "csrc", "fs_kernels.hip")
     text = open(src).read()
-    assert text.count("env_step<FM, P2, 11>") >= 3
+    assert text.count("env_step<FM, P2, 11, kTabLds, GEOM>") >= 3
     bad = tmp_path / "fs_kernels.hip"
-    bad.write_text(text.replace("env_step<FM, P2, 11>", "env_step<FM, P2, 30>"))
+    bad.write_text(text.replace("env_step<FM, P2, 11, kTabLds, GEOM>", "env_step<FM, P2, 30, kTabLds, GEOM>"))
     # the one-lane kernel (fs_arena1.h, included from the same directory) waits with
     # vmcnt(12 (D - 1)), D = 3 slots: 24 is exact, so 25 must be reported
     one = open(os.path.join(ROOT, "footsies_gym_amd", "csrc", "fs_arena1.h")).read()

@@ -5,7 +5,7 @@ import pytest
 
 from footsies_gym_amd import _abi
 from tests import golden_utils as gu
-from tests import kat_combat, kat_core
+from tests import kat_combat, kat_core, kat_geometry
 from tests import kat_scenarios as kat
 from tests import wire_client, wire_replay
 from tests import wrapper_replay as wr
@@ -31,6 +31,12 @@ def test_kat_combat_gpu(name):
 def test_kat_core_gpu(name):
     """tests/kat_core.py (the sim-core paths round 3 pinned only by lockstep) through the HIP path."""
     kat_core.ALL[name](SimBackend(1))
+
+
+@pytest.mark.parametrize("name", sorted(kat_geometry.ALL))
+def test_kat_geometry_gpu(name):
+    """tests/kat_geometry.py (the general-geometry tick: y != 0, flipped facings) through the HIP path."""
+    kat_geometry.ALL[name](SimBackend(1))
 
 
 @pytest.mark.parametrize("name", gu.CASES)

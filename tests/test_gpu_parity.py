@@ -176,3 +176,82 @@ def test_long_horizon_c3_size_matches_oracle(oracle_lib, p2):
     compare_outputs(ora.outputs(), sim.outputs_numpy())
     sim.close()
     ora.close()
+
+
+@pytest.mark.parametrize("p2,fm", [("external", "strict"), ("bot", "strict"), ("external", "double")])
+def test_lockstep_general_geometry(oracle_lib, p2, fm):
+    """STATE_LOAD of fighters off the ground (position.y != 0) and with flipped facings
+    (Fighter.LoadState F:741-744; the game itself never produces either) runs the kernels'
+    general-geometry tick -- box y extents from kRecY, y carried through both pushes (each push
+    adds a fighter's y to itself, BC:491-498, 511-515), mirrored boxes, movement and input
+    parsing -- against the oracle's direct restatement of the C#, one tick per launch, every
+    output and the full state (y and facing included) bit-exact; a round start clears both."""
+    n = 4096
+    sim, ora = make_pair(oracle_lib, n, p2, fm=fm, seed=41)
+    st = random_states(n, np.random.default_rng(141), p2=p2, geom_frac=0.3)
+    assert (st["f"]["position_y"] != 0).any() and (st["f"]["facing_flipped"] == 1).any()
+    assert ora.set_state(st) == 0
+    sim.set_state(st)
+    compare_states(ora.state(), sim.get_state(), step=-1)
+    run_lockstep(sim, ora, 200, np.random.default_rng(142), state_every=5, sticky=0.5)
+    end = sim.get_state()
+    y0, y1 = st["f"]["position_y"], end["f"]["position_y"]
+    moved = (y0 != 0) & (y1 != 0) & (y1 != y0)
+    assert moved.any(), "no push carried a y"                      # the doubling quirk ran
+    assert ((y0 != 0) & (y1 == 0)).any() and ((st["f"]["facing_flipped"] == 1) & (end["f"]["facing_flipped"] == 0)).any()
+
+
+@pytest.mark.parametrize("p2", ["external", "bot"])
+def test_fused_general_geometry_matches_oracle(oracle_lib, p2):
+    """The fused kernel's general-geometry loop (fs_step_n after such a load; the two-lane kernel
+    even where the one-lane one would run) against the oracle, every trajectory row and the final
+    state; then the hashed-action loop on top."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    N, T = 2999, 120
+    sim = FootsiesSim(N, p2_mode=p2, seed=7)
+    ora = oracle_lib.Oracle(N, p2_mode=P2[p2], base_seed=7)
+    st = random_states(N, np.random.default_rng(143), p2=p2, geom_frac=0.4)
+    assert ora.set_state(st) == 0
+    sim.set_state(st)
+    p1, p2a = sim.hash_actions(T, seed=93, p2=p2 == "external")
+    traj = sim.alloc_trajectory(T)
+    sim.step_n(T, p1, p2a if p2 == "external" else None, trajectory=traj)
+    torch.cuda.synchronize()
+    tr = {k: v.cpu().numpy() for k, v in traj.items()}
+    h1 = p1.cpu().numpy()
+    h2 = p2a.cpu().numpy() if p2 == "external" else None
+    for t in range(T):
+        exp = ora.step(h1[t], None if h2 is None else h2[t])
+        compare_outputs(exp, {k: v[t] for k, v in tr.items()}, step=t)
+    compare_states(ora.state(), sim.get_state())
+    sim.step_n(40, None, None, action_seed=0x6E0)
+    ora.step_n_hashed(40, 0x6E0)
+    torch.cuda.synchronize()
+    compare_states(ora.state(), sim.get_state())
+    compare_outputs(ora.outputs(), sim.outputs_numpy())
+
+
+def test_standard_load_leaves_the_general_geometry_path():
+    """fs_step_kernel names the kernel a launch runs: after a load with an airborne fighter the
+    fused launch at >= 131 072 arenas takes the two-lane kernel (the one-lane one has no general-
+    geometry tick); a later load of standard fighters only returns to the one-lane kernel."""
+    import os
+    from footsies_gym_amd._lib import lib
+    from footsies_gym_amd.simulator import FootsiesSim
+    if os.environ.get("FOOTSIES_FUSED_LANES"):
+        pytest.skip("the kernel choice is forced")
+    sim = FootsiesSim(131072, p2_mode="external", seed=3)
+    name = lambda: lib().fs_step_kernel(sim.handle, 100, 0).decode()  # noqa: E731
+    assert name() == "fsk::k_step_n1<0, 0>"
+    st = sim.get_state()
+    st["f"][5, 0]["position_y"] = np.float32(0.5)
+    sim.set_state(st)
+    assert name() == "fsk::k_step_n<0, 0>"
+    st["f"][5, 0]["position_y"] = np.float32(-0.0)  # -0.0 is ground level
+    sim.set_state(st)
+    assert name() == "fsk::k_step_n1<0, 0>"
+    st["f"][7, 1]["facing_flipped"] = 1
+    sim.set_state(st)
+    assert name() == "fsk::k_step_n<0, 0>"
+    sim.close()

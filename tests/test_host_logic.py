@@ -220,27 +220,38 @@ def _battle_state_doc():
     return B, st, B.battle_state(st, 0)
 
 
-def test_battle_state_load_rejects_airborne_or_flipped_fighters():
-    """Fighter.LoadState restores position.y and isFaceRight (Fighter.cs:741-744); the simulator
-    keeps y = 0 and the fixed facings, so a state with y != 0 or a flipped fighter is refused with
-    a FootsiesError (never continued as a different game).  The canonical state loads."""
+def test_battle_state_load_keeps_airborne_and_flipped_fighters():
+    """Fighter.LoadState restores position.y and isFaceRight (Fighter.cs:741-744): a loaded y and
+    a flipped facing land in position_y / facing_flipped, and the saved state gives them back with
+    every box at y + rect.y and mirrored in x (TransformToFightRect F:706-719).  A position that
+    is not [x, y] is refused (UnsupportedBattleStateError, a FootsiesError)."""
     from footsies_gym_amd._lib import FootsiesError
     B, st, doc = _battle_state_doc()
-    B.load_into(st.copy(), 0, B.dumps(doc))  # a state the game can produce loads
-    for who, field, value, msg in (("p1State", "position", [-2.0, 0.5], "position\\[1\\]"),
-                                   ("p2State", "position", [2.0, -1e-30], "position\\[1\\]"),
-                                   ("p1State", "isFaceRight", False, "isFaceRight"),
-                                   ("p2State", "isFaceRight", True, "isFaceRight"),
-                                   ("p1State", "position", [1.0], "position must be")):
-        bad = json.loads(B.dumps(doc))
-        bad[who][field] = value
-        with pytest.raises(FootsiesError, match=msg) as e:
-            B.load_into(st.copy(), 0, json.dumps(bad))
-        assert isinstance(e.value, ValueError) and e.value.code == _abi.FS_E_UNSUPPORTED
-    # -0.0 is ground level too
-    ok = json.loads(B.dumps(doc))
-    ok["p1State"]["position"] = [-2.0, -0.0]
-    B.load_into(st.copy(), 0, json.dumps(ok))
+    s0 = st.copy()
+    B.load_into(s0, 0, B.dumps(doc))  # a state the game can produce loads unchanged
+    assert s0[0]["f"][0]["position_y"] == 0 and s0[0]["f"][0]["facing_flipped"] == 0
+    alt = json.loads(B.dumps(doc))
+    alt["p1State"]["position"] = [-2.0, 0.5]
+    alt["p2State"]["isFaceRight"] = True
+    s1 = st.copy()
+    B.load_into(s1, 0, json.dumps(alt))
+    f1, f2 = s1[0]["f"][0], s1[0]["f"][1]
+    assert f1["position_y"] == np.float32(0.5) and f1["facing_flipped"] == 0
+    assert f2["position_y"] == 0 and f2["facing_flipped"] == 1
+    back = B.battle_state(s1, 0)
+    assert back["p1State"]["position"] == [-2.0, 0.5] and back["p1State"]["isFaceRight"] is True
+    assert back["p2State"]["isFaceRight"] is True
+    base = B.battle_state(st, 0)
+    for a, b in zip(back["p1State"]["hurtboxes"], base["p1State"]["hurtboxes"]):
+        assert a["y"] == float(np.float32(np.float32(0.5) + np.float32(b["y"]))) and a["x"] == b["x"]
+    for a, b in zip(back["p2State"]["hurtboxes"], base["p2State"]["hurtboxes"]):
+        # P2 at x = 2 facing right: x + rect.x instead of x - rect.x
+        assert a["x"] - 2.0 == pytest.approx(-(b["x"] - 2.0)) and a["y"] == b["y"]
+    bad = json.loads(B.dumps(doc))
+    bad["p1State"]["position"] = [1.0]
+    with pytest.raises(FootsiesError, match="position must be") as e:
+        B.load_into(st.copy(), 0, json.dumps(bad))
+    assert isinstance(e.value, ValueError) and e.value.code == _abi.FS_E_UNSUPPORTED
 
 
 def test_single_env_host_conversion_equals_batch_path():

@@ -2,7 +2,7 @@
 import pytest
 
 from footsies_gym_amd import _abi
-from tests import kat_actors, kat_combat, kat_core
+from tests import kat_actors, kat_combat, kat_core, kat_geometry
 from tests import kat_scenarios as kat
 
 
@@ -26,6 +26,12 @@ def test_kat_combat_oracle(oracle_lib, name):
 def test_kat_core_oracle(oracle_lib, name):
     """The sim-core paths pinned by hand-derived scenarios (tests/kat_core.py) on the oracle."""
     kat_core.ALL[name](kat_combat.OracleKat(oracle_lib))
+
+
+@pytest.mark.parametrize("name", sorted(kat_geometry.ALL))
+def test_kat_geometry_oracle(oracle_lib, name):
+    """Fighters off the ground / facing the other way (tests/kat_geometry.py) on the oracle."""
+    kat_geometry.ALL[name](kat_combat.OracleKat(oracle_lib))
 
 
 def test_kat_core_covers_its_pin_table():
