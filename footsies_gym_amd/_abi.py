@@ -93,6 +93,12 @@ OUTPUT_SPEC = {
 }
 
 
+class fs_host_arrays(C.Structure):
+    _fields_ = [(name, C.c_void_p) for name in (
+        "guard", "move", "move_frame", "position", "info_guard", "info_move", "info_move_frame", "info_position",
+        "frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun", "reward", "terminated", "truncated")]
+
+
 class fs_policy(C.Structure):
     _fields_ = [
         ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p), ("w3", C.c_void_p),
@@ -177,6 +183,7 @@ LIB_FUNCTIONS = {
     "fs_num_envs": (C.c_int, [C.c_void_p]),
     "fs_steps_taken": (C.c_uint64, [C.c_void_p]),
     "fs_step_kernel": (C.c_char_p, [C.c_void_p, C.c_int, C.c_int]),
+    "fs_host_convert": (C.c_int, [C.POINTER(fs_outputs), C.c_void_p, C.c_int64, C.POINTER(fs_host_arrays), C.c_int]),
     "fs_destroy": (None, [C.c_void_p]),
     "fs_last_error": (C.c_char_p, [C.c_void_p]),
 }

@@ -6,13 +6,19 @@
 // see fs_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
+#include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
-#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fs_internal.h"
@@ -785,3 +791,145 @@ FS_API void fs_destroy(fs_handle h) {
 }
 
 FS_API const char* fs_last_error(fs_handle h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+// ---------------------------------------------------------------------------
+// host-side conversion of a step's outputs (fs_host_convert)
+// ---------------------------------------------------------------------------
+namespace {
+// A fixed set of host worker threads, created on first use.  The pool object is never destroyed
+// (its workers sleep on a condition variable until the process exits), and a forked child gets
+// a fresh pool: the parent's workers do not exist there.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* pool = nullptr;
+    static pid_t owner = 0;
+    static std::mutex make;
+    std::lock_guard<std::mutex> g(make);
+    if (!pool || owner != getpid()) {
+      pool = new HostPool();  // (a pool inherited through fork is abandoned, not destroyed)
+      owner = getpid();
+    }
+    return *pool;
+  }
+  // fn(part, parts) for part = 0 .. parts - 1, part 0 on the calling thread; returns when all ran
+  void run(int parts, const std::function<void(int, int)>& fn) {
+    if (parts <= 1) {
+      fn(0, 1);
+      return;
+    }
+    std::lock_guard<std::mutex> serial(run_m_);  // one job at a time
+    {
+      std::lock_guard<std::mutex> g(m_);
+      while ((int)workers_.size() < parts - 1) {
+        const int id = (int)workers_.size();
+        workers_.push_back(new std::thread([this, id] { loop(id); }));
+      }
+      fn_ = &fn;
+      parts_ = parts;
+      left_ = parts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0, parts);
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(int id) {  // worker id runs part id + 1 of the jobs that have that many parts
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (id + 1 >= parts_) continue;
+      const std::function<void(int, int)>* fn = fn_;
+      const int parts = parts_;
+      g.unlock();
+      (*fn)(id + 1, parts);
+      g.lock();
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex m_, run_m_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread*> workers_;
+  const std::function<void(int, int)>* fn_ = nullptr;
+  int parts_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+};
+}  // namespace
+
+FS_API int fs_host_convert(const fs_outputs* src, const int64_t* rows, int64_t n, const fs_host_arrays* dst,
+                           int threads) {
+  if (!src || !dst || n < 0) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: src, dst and n >= 0 required");
+  const fs_outputs S = *src;
+  const fs_host_arrays D = *dst;
+  if ((D.guard || D.info_guard) && !S.guard) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: no guard source");
+  if ((D.move || D.info_move) && !S.move) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: no move source");
+  if ((D.move_frame || D.info_move_frame) && !S.move_frame)
+    return set_err(nullptr, FS_E_INVALID, "fs_host_convert: no move_frame source");
+  if ((D.position || D.info_position) && !S.position)
+    return set_err(nullptr, FS_E_INVALID, "fs_host_convert: no position source");
+  if ((D.frame && !S.frame) || ((D.p1_action || D.p2_action) && !S.action) ||
+      ((D.p1_hitstun || D.p2_hitstun) && !S.hitstun) || (D.reward && !S.reward) ||
+      (D.terminated && !S.terminated) || (D.truncated && !S.truncated))
+    return set_err(nullptr, FS_E_INVALID, "fs_host_convert: a destination without its source");
+  // below ~8k rows the threads' wake-up costs more than the conversion
+  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(threads, 1), n / 8192 + 1, 64}));
+  HostPool::get().run(parts, [&](int part, int np) {
+    const int64_t lo = n * part / np, hi = n * (part + 1) / np;
+    // field by field over this part's rows (contiguous loops the compiler vectorizes); row r of
+    // the source is rows[i] or i
+    auto pairs = [&](auto* d, const auto* sp) {  // [N][2] -> [n][2]
+      if (!d) return;
+      if (!rows) {
+        for (int64_t j = 2 * lo; j < 2 * hi; ++j) d[j] = sp[j];
+      } else {
+        for (int64_t i = lo; i < hi; ++i) {
+          d[2 * i] = sp[2 * rows[i]];
+          d[2 * i + 1] = sp[2 * rows[i] + 1];
+        }
+      }
+    };
+    auto single = [&](auto* d, const auto* sp, int stride, int k) {  // column k of [N][stride] -> [n]
+      if (!d) return;
+      if (!rows) {
+        for (int64_t i = lo; i < hi; ++i) d[i] = sp[stride * i + k];
+      } else {
+        for (int64_t i = lo; i < hi; ++i) d[i] = sp[stride * rows[i] + k];
+      }
+    };
+    pairs(D.guard, S.guard);
+    pairs(D.info_guard, S.guard);
+    pairs(D.move, S.move);
+    pairs(D.info_move, S.move);
+    pairs(D.move_frame, S.move_frame);
+    pairs(D.info_move_frame, S.move_frame);
+    pairs(D.position, S.position);
+    pairs(D.info_position, S.position);
+    single(D.frame, S.frame, 1, 0);
+    single(D.p1_hitstun, S.hitstun, 2, 0);
+    single(D.p2_hitstun, S.hitstun, 2, 1);
+    single(D.reward, S.reward, 1, 0);
+    for (int k = 0; k < 2; ++k) {
+      uint8_t* act = k == 0 ? D.p1_action : D.p2_action;
+      if (!act) continue;
+      for (int64_t i = lo; i < hi; ++i) {
+        const uint8_t a = S.action[2 * (rows ? rows[i] : i) + k];  // Left = 1, Right = 2, Attack = 4 (state.py:26-36)
+        act[3 * i] = a & 1;
+        act[3 * i + 1] = (a >> 1) & 1;
+        act[3 * i + 2] = (a >> 2) & 1;
+      }
+    }
+    for (int k = 0; k < 2; ++k) {
+      uint8_t* d = k == 0 ? D.terminated : D.truncated;
+      const uint8_t* sp = k == 0 ? S.terminated : S.truncated;
+      if (!d) continue;
+      for (int64_t i = lo; i < hi; ++i) d[i] = sp[rows ? rows[i] : i] != 0;
+    }
+  });
+  return FS_OK;
+}

@@ -13,11 +13,13 @@ Differences from the reference, by design:
     SyncVectorEnv (returned obs is the new episode's first obs, the terminal one
     is in ``infos["final_observation"]``); ``"next_step"`` follows gymnasium 1.x.
 """
+import ctypes as C
+
 import numpy as np
 
 from . import _abi, battle_state
 from . import spaces as sp
-from ._lib import FootsiesGameClosedError
+from ._lib import FootsiesGameClosedError, check, lib
 from .simulator import FootsiesSim, decode_actions, encode_actions
 
 try:  # pragma: no cover - depends on the environment
@@ -58,9 +60,73 @@ def retain_host_heap():
     return _HEAP_RETAINED
 
 
+_SRC_DTYPES = {"guard": np.uint8, "move": np.uint8, "move_frame": np.float32, "position": np.float32,
+               "reward": np.float64, "terminated": np.uint8, "truncated": np.uint8, "frame": np.int32,
+               "action": np.uint8, "hitstun": np.uint8}
+_HOST_THREADS = None
+
+
+def host_threads():
+    """Host threads fs_host_convert splits a step's conversion over: FOOTSIES_HOST_THREADS, else
+    up to 8 of the process's CPUs."""
+    global _HOST_THREADS
+    if _HOST_THREADS is None:
+        import os
+        env = os.environ.get("FOOTSIES_HOST_THREADS")
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            avail = os.cpu_count() or 1
+        _HOST_THREADS = max(1, int(env)) if env else max(1, min(8, avail))
+    return _HOST_THREADS
+
+
+def _host_convert(out, prefix, rows, n, want_step):
+    """(obs, info[, reward, terminated, truncated]) of n rows of host outputs through
+    fs_host_convert (one pass over the rows on the library's host threads)."""
+    keep = []
+
+    def src(name):
+        a = np.ascontiguousarray(out[prefix + name], dtype=_SRC_DTYPES[name])
+        keep.append(a)
+        return a.ctypes.data
+    names = ("guard", "move", "move_frame", "position", "frame", "action", "hitstun")
+    so = _abi.fs_outputs(**{k: src(k) for k in names})
+    obs = {"guard": np.empty((n, 2), np.int64), "move": np.empty((n, 2), np.int64),
+           "move_frame": np.empty((n, 2), np.float32), "position": np.empty((n, 2), np.float32)}
+    copies = {k: np.empty_like(v) for k, v in obs.items()}  # FE:379 puts a copy of the obs in the info
+    info = {"frame": np.empty(n, np.int64), "p1_action": np.empty((n, 3), np.bool_),
+            "p2_action": np.empty((n, 3), np.bool_), "p1_hitstun": np.empty(n, np.int64),
+            "p2_hitstun": np.empty(n, np.int64)}
+    d = dict(guard=obs["guard"], move=obs["move"], move_frame=obs["move_frame"], position=obs["position"],
+             info_guard=copies["guard"], info_move=copies["move"], info_move_frame=copies["move_frame"],
+             info_position=copies["position"], frame=info["frame"], p1_action=info["p1_action"],
+             p2_action=info["p2_action"], p1_hitstun=info["p1_hitstun"], p2_hitstun=info["p2_hitstun"])
+    extra = None
+    if want_step:
+        so.reward, so.terminated, so.truncated = src("reward"), src("terminated"), src("truncated")
+        extra = (np.empty(n, np.float64), np.empty(n, np.bool_), np.empty(n, np.bool_))
+        d.update(reward=extra[0], terminated=extra[1], truncated=extra[2])
+    dst = _abi.fs_host_arrays(**{k: v.ctypes.data for k, v in d.items()})
+    r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
+    check(lib().fs_host_convert(C.byref(so), None if r is None else C.c_void_p(r.ctypes.data), n, C.byref(dst),
+                                host_threads()))
+    info.update(copies)
+    return obs, info, extra
+
+
 def obs_info_from_outputs(out, prefix=""):
     """Host-side view of one set of kernel outputs -> (obs, info) batches with the
-    reference dtypes: MultiDiscrete -> int64, Box -> float32 (FE:157-168, 336-380)."""
+    reference dtypes: MultiDiscrete -> int64, Box -> float32 (FE:157-168, 336-380); converted
+    by fs_host_convert (obs_info_from_outputs_numpy is the same in numpy)."""
+    n = len(out[prefix + "frame"])
+    obs, info, _ = _host_convert(out, prefix, None, n, False)
+    return obs, info
+
+
+def obs_info_from_outputs_numpy(out, prefix=""):
+    """obs_info_from_outputs written with numpy ops (the reference the native conversion is
+    tested against)."""
     obs = {  # (always new arrays: ``out`` may be views of a reused host buffer)
         "guard": np.array(out[prefix + "guard"], dtype=np.int64),
         "move": np.array(out[prefix + "move"], dtype=np.int64),
@@ -81,16 +147,14 @@ def obs_info_from_outputs(out, prefix=""):
 
 
 def step_result_from_outputs(out, autoreset_mode="same_step"):
-    """(obs, rewards, terminations, truncations, infos) from host copies of the outputs."""
-    obs, info = obs_info_from_outputs(out)
-    rewards = np.array(out["reward"], dtype=np.float64)
-    term = np.asarray(out["terminated"]).astype(bool)
-    trunc = np.asarray(out["truncated"]).astype(bool)
+    """(obs, rewards, terminations, truncations, infos) from host copies of the outputs: one
+    fs_host_convert pass over all rows, and one over the terminated arenas' final records."""
+    n = len(out["frame"])
+    obs, info, (rewards, term, trunc) = _host_convert(out, "", None, n, True)
     if autoreset_mode == "same_step" and term.any():
         idx = np.nonzero(term)[0]
         # only the terminated arenas' final outputs are converted
-        fobs, finfo = obs_info_from_outputs({k: v[idx] for k, v in out.items() if k.startswith("final_")},
-                                            prefix="final_")
+        fobs, finfo, _ = _host_convert(out, "final_", idx, len(idx), False)
         final_obs = np.empty(len(term), dtype=object)
         final_info = np.empty(len(term), dtype=object)
         # Per-arena dicts (gymnasium 0.29's contract: one dict per terminated env, None elsewhere),

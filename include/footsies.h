@@ -355,6 +355,37 @@ int fs_hash_actions(fs_handle h, int n_steps, uint64_t seed, uint64_t t0, uint8_
 /* Device pointers of the current outputs, valid until the next call on h. */
 int fs_outputs_get(fs_handle h, fs_outputs* out);
 
+/* The host arrays of one FootsiesVectorEnv numpy step (vector_env.step_result_from_outputs, the
+ * batched form of FE:336-380's _extract_obs / _extract_info and FE:555-570), in the reference's
+ * dtypes: Gymnasium's MultiDiscrete as int64, Box as float32, bools as 0 / 1 bytes.  Any member
+ * may be NULL (not written).  [N][2] arrays are P1, P2 per row; *_action are [N][3] (Left, Right,
+ * Attack; state.py:26-36). */
+typedef struct fs_host_arrays {
+  int64_t* guard;            /* obs["guard"]      [N][2] */
+  int64_t* move;             /* obs["move"]       [N][2] */
+  float* move_frame;         /* obs["move_frame"] [N][2] */
+  float* position;           /* obs["position"]   [N][2] */
+  int64_t* info_guard;       /* the info's copies of the observation (FE:379) */
+  int64_t* info_move;
+  float* info_move_frame;
+  float* info_position;
+  int64_t* frame;            /* info["frame"]      [N] */
+  uint8_t* p1_action;        /* info["p1_action"]  [N][3] bool */
+  uint8_t* p2_action;        /* info["p2_action"]  [N][3] bool */
+  int64_t* p1_hitstun;       /* info["p1_hitstun"] [N] */
+  int64_t* p2_hitstun;       /* info["p2_hitstun"] [N] */
+  double* reward;            /* [N] */
+  uint8_t* terminated;       /* [N] bool */
+  uint8_t* truncated;        /* [N] bool */
+} fs_host_arrays;
+
+/* Convert host copies of step outputs (`src`: the fs_outputs layout in host memory, e.g. the
+ * pinned copy of fs_outputs_get's buffers; only its first ten members are read) into `dst`,
+ * over `threads` host threads (a pool kept by the library).  Row i of dst is row rows[i] of src
+ * (rows NULL: row i), for i < n -- so the terminal records of the arenas that ended a step are
+ * converted by passing the final_* arrays as src's first members and the terminated rows. */
+int fs_host_convert(const fs_outputs* src, const int64_t* rows, int64_t n, const fs_host_arrays* dst, int threads);
+
 /* Pack the current outputs into one FS_RECORD_BYTES record per arena at dst (device,
  * [N][40] bytes): guard[2] move[2] action[2] hitstun[2] u8, terminated u8, truncated
  * u8, pad[2], move_frame[2] f32, position[2] f32, frame i32, reward f64 -- the payload

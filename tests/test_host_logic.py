@@ -287,3 +287,43 @@ def test_retain_host_heap_is_opt_out_and_idempotent():
     env = dict(os.environ, FOOTSIES_NO_MALLOPT="1")
     off = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True, env=env).stdout.split()
     assert off == ["False", "False"]
+
+
+@pytest.mark.parametrize("n,threads", [(1, 1), (7, 4), (20000, 3), (65536, 8)])
+def test_native_host_conversion_equals_numpy(n, threads, monkeypatch):
+    """fs_host_convert (the library's threaded host conversion behind FootsiesVectorEnv's numpy
+    step) gives exactly the arrays, dtypes and shapes of the numpy formulation, for all rows and
+    for a row selection (the terminated arenas' final records), over several thread counts."""
+    from footsies_gym_amd import vector_env as V
+    monkeypatch.setattr(V, "_HOST_THREADS", threads)
+    rng = np.random.default_rng(n)
+    out = {}
+    for pre in ("", "final_"):
+        out[pre + "guard"] = rng.integers(0, 4, (n, 2)).astype(np.uint8)
+        out[pre + "move"] = rng.integers(0, 17, (n, 2)).astype(np.uint8)
+        out[pre + "move_frame"] = rng.integers(0, 60, (n, 2)).astype(np.float32)
+        out[pre + "position"] = (rng.standard_normal((n, 2)) * 3).astype(np.float32)
+        out[pre + "action"] = rng.integers(0, 8, (n, 2)).astype(np.uint8)
+        out[pre + "hitstun"] = rng.integers(0, 30, (n, 2)).astype(np.uint8)
+        out[pre + "frame"] = rng.integers(-1, 3000, n).astype(np.int32)
+    out["reward"] = rng.standard_normal(n)
+    out["terminated"] = (rng.random(n) < 0.3).astype(np.uint8)
+    out["truncated"] = np.zeros(n, np.uint8)
+    obs, info = V.obs_info_from_outputs(out)
+    eobs, einfo = V.obs_info_from_outputs_numpy(out)
+    for a, b in ((obs, eobs), (info, einfo)):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert a[k].dtype == b[k].dtype and a[k].shape == b[k].shape and np.array_equal(a[k], b[k]), k
+    # the info's observation entries are copies, not the obs arrays themselves (FE:379)
+    assert all(info[k] is not obs[k] and not np.shares_memory(info[k], obs[k]) for k in obs)
+    o, r, t, tr, i = V.step_result_from_outputs(out)
+    assert r.dtype == np.float64 and np.array_equal(r, out["reward"]) and t.dtype == np.bool_
+    assert np.array_equal(t, out["terminated"] != 0) and not tr.any()
+    idx = np.nonzero(out["terminated"])[0]
+    for j in idx[:50]:
+        fo, fi = i["final_observation"][j], i["final_info"][j]
+        assert np.array_equal(fo["guard"], out["final_guard"][j].astype(np.int64))
+        assert np.array_equal(fi["p2_action"], [bool(out["final_action"][j, 1] & b) for b in (1, 2, 4)])
+        assert fi["frame"] == out["final_frame"][j] and fi["p1_hitstun"] == out["final_hitstun"][j, 0]
+    assert all(i["final_observation"][j] is None for j in np.nonzero(out["terminated"] == 0)[0][:50])

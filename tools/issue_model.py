@@ -59,17 +59,24 @@ def kernel_insts(dis, name):
 
 
 def main_loop(insts):
-    """[start, end] indices of the backward branch spanning the most instructions."""
+    """[start, end] indices of the standard tick loop: the backward branch spanning the most
+    instructions among those whose body loads nothing 16 bytes wide from global memory.  (Since
+    round 4 each fused kernel holds two tick loops, the standard one and the general-geometry
+    one, which reads the boxes' y extents from kRecY.)"""
     addr = {a: i for i, (a, *_rest) in enumerate(insts)}
-    best = None
+    loops = []
     for i, (a, mn, ops, size) in enumerate(insts):
         if mn.startswith("s_cbranch") or mn == "s_branch":
             off = int(ops.split()[0])
             off = off - 65536 if off >= 32768 else off
             tgt = a + 4 + 4 * off
-            if off < 0 and tgt in addr and (best is None or i - addr[tgt] > best[1] - best[0]):
-                best = (addr[tgt], i)
-    return best
+            if off < 0 and tgt in addr:
+                loops.append((addr[tgt], i))
+    # the general-geometry loop reads kRecY (global_load_dwordx4); the standard tick has no 16-byte
+    # global loads (its tables are in LDS, its row loads single bytes)
+    std = [lp for lp in loops if not any(insts[j][1] == "global_load_dwordx4" for j in range(lp[0], lp[1] + 1))]
+    pool = std or loops
+    return max(pool, key=lambda lp: lp[1] - lp[0]) if pool else None
 
 
 def reads_vcc(mn, ops):
