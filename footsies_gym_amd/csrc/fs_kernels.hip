@@ -1137,10 +1137,11 @@ __device__ __forceinline__ void end_tick(Fighter& f, bool won) {
 }
 
 // SetupBattleStart (F:120-135): hitstun and the two guard latches are NOT reset
+// (position.y = 0 and isFaceRight = isPlayerOne, F:123-124, BC:264-265, are set by the callers
+// that carry them: the general-geometry tick and the reset kernel; on the standard tick both
+// already hold.)
 __device__ __forceinline__ void setup_battle_start(Fighter& f, float x) {
   f.x = x;
-  f.y = 0.0f;   // position = startPosition (x, 0) (BC:264-265)
-  f.flip = 0;   // isFaceRight = isPlayerOne (F:124)
   f.vital = 1;
   f.guard = kStartGuard;
   f.won = false;
@@ -1388,6 +1389,10 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   const Actors ac{p.p1_bot != 0, p.p2_resets != 0, p.p2_noop != 0};
   if (L.pending) {  // FS_AUTORESET_NEXT_STEP: this step runs the reset burst only
     reset_burst<FM, P2, G>(L, true, ac);
+    if constexpr (GEOM) {  // the round start's position (x, 0) and facing (F:123-124)
+      L.f.y = 0.0f;
+      L.f.flip = 0;
+    }
     L.pending = false;
     L.has_term = false;
     L.cum = 0.0;
@@ -1499,6 +1504,10 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     if (p.autoreset_mode == FS_AUTORESET_SAME_STEP) {
       write_final(L, o, r);
       reset_burst<FM, P2, G>(L, true, ac);
+      if constexpr (GEOM) {
+        L.f.y = 0.0f;
+        L.f.flip = 0;
+      }
       L.cum = 0.0;
       L.has_term = false;
       L.ai = stand_info();  // the burst ends on STAND
@@ -1803,8 +1812,14 @@ __global__ __launch_bounds__(256) void k_reset(ResetParams p) {
   if (L.pending) {  // finish the burst Unity ran after the terminal frame
     reset_burst<FM, kActors>(L, true, ac);
     L.pending = false;
+    L.f.y = 0.0f;  // the round start's position (x, 0) and facing (F:123-124)
+    L.f.flip = 0;
   }
-  if (hard) reset_burst<FM, kActors>(L, false, ac);
+  if (hard) {
+    reset_burst<FM, kActors>(L, false, ac);
+    L.f.y = 0.0f;
+    L.f.flip = 0;
+  }
   L.cum = 0.0;
   L.has_term = p.init ? true : false;
   write_main(L, p.out, a);
