@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def kernel_resources(src, extra=()):
     """{kernel symbol: {"VGPRs": .., "ScratchSize": .., "Occupancy": ..}} from the compiler's remarks."""
-    cmd = [B._hipcc(), "--offload-arch=" + B.ARCH, *B.CFLAGS, *extra, "-I", os.path.join(ROOT, "include"),
+    cmd = [B._hipcc(), "--offload-arch=" + B.ARCH, *B.flags_for(src), *extra, "-I", os.path.join(ROOT, "include"),
            "--cuda-device-only", "-S", "-o", os.devnull, os.path.join(B.CSRC, src),
            "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)

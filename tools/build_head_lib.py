@@ -32,7 +32,7 @@ def main(rev, out):
     objs = []
     for s in B.SOURCES:
         o = os.path.join(out, s + ".o")
-        subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.CFLAGS, "-I", inc,
+        subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.flags_for(s), "-I", inc,
                         "-c", os.path.join(src, s), "-o", o], check=True)
         objs.append(o)
     subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, "-shared", "-fPIC", "-o",

@@ -25,7 +25,7 @@ def main(src, out, extra=()):
     objs = []
     for s in B.SOURCES:
         o = os.path.join(out, s + ".o")
-        subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.CFLAGS, *extra, "-I", os.path.join(ROOT, "include"),
+        subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.flags_for(s), *extra, "-I", os.path.join(ROOT, "include"),
                         "-c", os.path.join(out, s), "-o", o], check=True)
         objs.append(o)
     subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, "-shared", "-fPIC", "-o",

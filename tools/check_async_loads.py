@@ -300,7 +300,7 @@ def main():
     from footsies_gym_amd import build as B
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "k.s")
-        subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.CFLAGS, *extra, "-I", os.path.join(ROOT, "include"),
+        subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.flags_for(src), *extra, "-I", os.path.join(ROOT, "include"),
                         "-I", B.CSRC, "--cuda-device-only", "-S", "-o", out, src], check=True,
                        stderr=subprocess.DEVNULL)
         asm = open(out).read()

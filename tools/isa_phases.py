@@ -93,7 +93,7 @@ HELPERS = {"xpair", "xp1", "xp2", "fadd", "fsub", "fadd2", "fsub2", "tabs", "bit
 
 def compile_debug(src, out_dir):
     co = os.path.join(out_dir, "k.co")
-    subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.CFLAGS, "-gline-tables-only", "-I",
+    subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.flags_for(src), "-gline-tables-only", "-I",
                     os.path.join(ROOT, "include"), "--cuda-device-only", "-c", "-o", co, src], check=True)
     dev = os.path.join(out_dir, "k.gfx950.o")
     subprocess.run([LLVM + "/clang-offload-bundler", "--type=o", "--input=" + co,
@@ -216,7 +216,7 @@ def main():
         rows.append(row)
         (rare if row["rare"] else common).update(c)
     rows.sort(key=lambda r: (r["rare"], -r["per_tick"].get("valu", 0), -r["total_per_tick"]))
-    res = {"kernel": a.kernel, "source": os.path.relpath(a.src, ROOT), "flags": "build.py CFLAGS + -gline-tables-only "
+    res = {"kernel": a.kernel, "source": os.path.relpath(a.src, ROOT), "flags": "build.py flags_for(fs_kernels.hip) + -gline-tables-only "
            "(same code as the library: mnemonic sequence checked)",
            "loop_instructions": len(loop), "ticks_in_loop": ticks,
            "common_path_per_tick": {k: v / ticks for k, v in sorted(common.items())},

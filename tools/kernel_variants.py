@@ -88,7 +88,7 @@ def build():
         objs = []
         for s in B.SOURCES:
             o = os.path.join(d, s + ".o")
-            subprocess.run([B._hipcc(), "--offload-arch=gfx950", *B.CFLAGS, "-I", os.path.join(ROOT, "include"),
+            subprocess.run([B._hipcc(), "--offload-arch=gfx950", *B.flags_for(s), "-I", os.path.join(ROOT, "include"),
                             "-I", CSRC, "-c", os.path.join(d, s), "-o", o], check=True)
             objs.append(o)
         subprocess.run([B._hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
