@@ -81,37 +81,63 @@ def host_threads():
     return _HOST_THREADS
 
 
+# The destination arrays of one conversion, in the fs_host_arrays member order: (member, dtype,
+# columns); all of them are views of one fresh block (one allocation and one pointer per call).
+_DST = (("guard", np.int64, 2), ("move", np.int64, 2), ("move_frame", np.float32, 2), ("position", np.float32, 2),
+        ("info_guard", np.int64, 2), ("info_move", np.int64, 2), ("info_move_frame", np.float32, 2),
+        ("info_position", np.float32, 2), ("frame", np.int64, 0), ("p1_action", np.bool_, 3),
+        ("p2_action", np.bool_, 3), ("p1_hitstun", np.int64, 0), ("p2_hitstun", np.int64, 0),
+        ("reward", np.float64, 0), ("terminated", np.bool_, 0), ("truncated", np.bool_, 0))
+_SRC_NAMES = ("guard", "move", "move_frame", "position", "frame", "action", "hitstun")
+_PTRS = {}  # id(source array) -> (weak reference, data pointer): the sim's pinned views repeat every step
+
+
+def _src_ptr(a):
+    import weakref
+    hit = _PTRS.get(id(a))
+    if hit is not None and hit[0]() is a:
+        return hit[1]
+    p = a.ctypes.data
+    try:
+        _PTRS[id(a)] = (weakref.ref(a), p)
+    except TypeError:
+        pass
+    return p
+
+
 def _host_convert(out, prefix, rows, n, want_step):
-    """(obs, info[, reward, terminated, truncated]) of n rows of host outputs through
+    """(obs, info[, (reward, terminated, truncated)]) of n rows of host outputs through
     fs_host_convert (one pass over the rows on the library's host threads)."""
     keep = []
 
     def src(name):
-        a = np.ascontiguousarray(out[prefix + name], dtype=_SRC_DTYPES[name])
-        keep.append(a)
-        return a.ctypes.data
-    names = ("guard", "move", "move_frame", "position", "frame", "action", "hitstun")
-    so = _abi.fs_outputs(**{k: src(k) for k in names})
-    obs = {"guard": np.empty((n, 2), np.int64), "move": np.empty((n, 2), np.int64),
-           "move_frame": np.empty((n, 2), np.float32), "position": np.empty((n, 2), np.float32)}
-    copies = {k: np.empty_like(v) for k, v in obs.items()}  # FE:379 puts a copy of the obs in the info
-    info = {"frame": np.empty(n, np.int64), "p1_action": np.empty((n, 3), np.bool_),
-            "p2_action": np.empty((n, 3), np.bool_), "p1_hitstun": np.empty(n, np.int64),
-            "p2_hitstun": np.empty(n, np.int64)}
-    d = dict(guard=obs["guard"], move=obs["move"], move_frame=obs["move_frame"], position=obs["position"],
-             info_guard=copies["guard"], info_move=copies["move"], info_move_frame=copies["move_frame"],
-             info_position=copies["position"], frame=info["frame"], p1_action=info["p1_action"],
-             p2_action=info["p2_action"], p1_hitstun=info["p1_hitstun"], p2_hitstun=info["p2_hitstun"])
-    extra = None
+        a = out[prefix + name]
+        if not (isinstance(a, np.ndarray) and a.dtype == _SRC_DTYPES[name] and a.flags.c_contiguous):
+            a = np.ascontiguousarray(a, dtype=_SRC_DTYPES[name])
+            keep.append(a)
+            return a.ctypes.data
+        return _src_ptr(a)
+    so = _abi.fs_outputs(**{k: src(k) for k in _SRC_NAMES})
     if want_step:
         so.reward, so.terminated, so.truncated = src("reward"), src("terminated"), src("truncated")
-        extra = (np.empty(n, np.float64), np.empty(n, np.bool_), np.empty(n, np.bool_))
-        d.update(reward=extra[0], terminated=extra[1], truncated=extra[2])
-    dst = _abi.fs_host_arrays(**{k: v.ctypes.data for k, v in d.items()})
+    members = _DST if want_step else _DST[:13]
+    sizes = [n * max(c, 1) * np.dtype(dt).itemsize for _, dt, c in members]
+    offs = np.concatenate(([0], np.cumsum([(b + 63) & ~63 for b in sizes])))  # 64-B aligned views
+    block = np.empty(int(offs[-1]) or 1, np.uint8)
+    base = block.ctypes.data
+    views, ptrs = {}, {}
+    for (name, dt, c), off, nb in zip(members, offs, sizes):
+        v = block[off:off + nb].view(dt)
+        views[name] = v.reshape(n, c) if c else v
+        ptrs[name] = base + int(off)
+    dst = _abi.fs_host_arrays(**ptrs)
     r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
     check(lib().fs_host_convert(C.byref(so), None if r is None else C.c_void_p(r.ctypes.data), n, C.byref(dst),
                                 host_threads()))
-    info.update(copies)
+    obs = {k: views[k] for k in ("guard", "move", "move_frame", "position")}
+    info = {k: views[k] for k in ("frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun")}
+    info.update({k: views["info_" + k] for k in ("guard", "move", "move_frame", "position")})  # FE:379's copies
+    extra = (views["reward"], views["terminated"], views["truncated"]) if want_step else None
     return obs, info, extra
 
 
