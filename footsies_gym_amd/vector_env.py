@@ -89,51 +89,57 @@ _DST = (("guard", np.int64, 2), ("move", np.int64, 2), ("move_frame", np.float32
         ("p2_action", np.bool_, 3), ("p1_hitstun", np.int64, 0), ("p2_hitstun", np.int64, 0),
         ("reward", np.float64, 0), ("terminated", np.bool_, 0), ("truncated", np.bool_, 0))
 _SRC_NAMES = ("guard", "move", "move_frame", "position", "frame", "action", "hitstun")
-_PTRS = {}  # id(source array) -> (weak reference, data pointer): the sim's pinned views repeat every step
+_STEP_NAMES = ("reward", "terminated", "truncated")
+# (member, dtype, columns, bytes per row) of the destination members, in _DST order
+_DST_ROWS = tuple((name, np.dtype(dt), c, np.dtype(dt).itemsize * max(c, 1)) for name, dt, c in _DST)
+# (prefix, want_step) -> (weak references to the source arrays, their fs_outputs): the sim's pinned
+# views are the same arrays every step, so their struct is built once
+_SRC_STRUCTS = {}
 
 
-def _src_ptr(a):
+def _src_struct(out, prefix, want_step):
+    """fs_outputs over the source arrays of one conversion, and the converted copies it points into
+    (to be kept alive over the call) when some source was not a C-contiguous array of its dtype."""
     import weakref
-    hit = _PTRS.get(id(a))
-    if hit is not None and hit[0]() is a:
-        return hit[1]
-    p = a.ctypes.data
-    try:
-        _PTRS[id(a)] = (weakref.ref(a), p)
-    except TypeError:
-        pass
-    return p
+    arrs = [out[prefix + k] for k in _SRC_NAMES]
+    if want_step:
+        arrs += [out[k] for k in _STEP_NAMES]  # (step outputs carry no final_ variant)
+    hit = _SRC_STRUCTS.get((prefix, want_step))
+    if hit is not None and len(hit[0]) == len(arrs) and all(w() is a for w, a in zip(hit[0], arrs)):
+        return hit[1], None
+    keep, ptrs = [], {}
+    for name, a in zip(_SRC_NAMES + (_STEP_NAMES if want_step else ()), arrs):
+        if not (isinstance(a, np.ndarray) and a.dtype == _SRC_DTYPES[name] and a.flags.c_contiguous):
+            a = np.ascontiguousarray(a, dtype=_SRC_DTYPES[name])
+            keep.append(a)
+        ptrs[name] = a.ctypes.data
+    so = _abi.fs_outputs(**ptrs)
+    if not keep:
+        try:
+            _SRC_STRUCTS[(prefix, want_step)] = (tuple(weakref.ref(a) for a in arrs), so)
+        except TypeError:  # (an ndarray subclass without weak references: not cached)
+            pass
+    return so, keep
 
 
 def _host_convert(out, prefix, rows, n, want_step):
     """(obs, info[, (reward, terminated, truncated)]) of n rows of host outputs through
     fs_host_convert (one pass over the rows on the library's host threads)."""
-    keep = []
-
-    def src(name):
-        a = out[prefix + name]
-        if not (isinstance(a, np.ndarray) and a.dtype == _SRC_DTYPES[name] and a.flags.c_contiguous):
-            a = np.ascontiguousarray(a, dtype=_SRC_DTYPES[name])
-            keep.append(a)
-            return a.ctypes.data
-        return _src_ptr(a)
-    so = _abi.fs_outputs(**{k: src(k) for k in _SRC_NAMES})
-    if want_step:
-        so.reward, so.terminated, so.truncated = src("reward"), src("terminated"), src("truncated")
-    members = _DST if want_step else _DST[:13]
-    sizes = [n * max(c, 1) * np.dtype(dt).itemsize for _, dt, c in members]
-    offs = np.concatenate(([0], np.cumsum([(b + 63) & ~63 for b in sizes])))  # 64-B aligned views
-    block = np.empty(int(offs[-1]) or 1, np.uint8)
+    so, keep = _src_struct(out, prefix, want_step)
+    members = _DST_ROWS if want_step else _DST_ROWS[:13]
+    offs, total = [], 0
+    for m in members:  # 64-B aligned members of one block
+        offs.append(total)
+        total += (n * m[3] + 63) & ~63
+    block = np.empty(total or 1, np.uint8)
     base = block.ctypes.data
-    views, ptrs = {}, {}
-    for (name, dt, c), off, nb in zip(members, offs, sizes):
-        v = block[off:off + nb].view(dt)
-        views[name] = v.reshape(n, c) if c else v
-        ptrs[name] = base + int(off)
-    dst = _abi.fs_host_arrays(**ptrs)
+    dst = _abi.fs_host_arrays(*[base + off for off in offs])
+    views = {name: np.ndarray((n, c) if c else (n,), dt, block, off)
+             for (name, dt, c, _), off in zip(members, offs)}
     r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
-    check(lib().fs_host_convert(C.byref(so), None if r is None else C.c_void_p(r.ctypes.data), n, C.byref(dst),
+    check(lib().fs_host_convert(C.byref(so), None if r is None else r.ctypes.data, n, C.byref(dst),
                                 host_threads()))
+    del keep  # (the converted sources lived over the call)
     obs = {k: views[k] for k in ("guard", "move", "move_frame", "position")}
     info = {k: views[k] for k in ("frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun")}
     info.update({k: views["info_" + k] for k in ("guard", "move", "move_frame", "position")})  # FE:379's copies
@@ -216,8 +222,10 @@ class FootsiesVectorEnv(_VectorEnvBase):
     ``by_example`` (FE:83-84, 118, 230-232): the in-game bot plays P1 as well and the agent only
     observes -- ``step`` ignores its actions (FE:522-523).
     ``output="torch"`` returns device tensors (zero-copy) instead of numpy.
-    (``_host_outputs``, internal: the kernels write the outputs into pinned host memory --
-    FootsiesSim ``host_outputs`` -- for the one-arena FootsiesEnv; numpy output only.)
+    (``_host_outputs``, internal, numpy output only: the kernels write the outputs into pinned host
+    memory -- FootsiesSim ``host_outputs`` -- instead of HBM, so a step needs no device-to-host copy
+    of its own.  The default for numpy output: at 65 536 arenas a step took 0.45-0.46 ms so, against
+    0.50-0.51 ms with the outputs in HBM and one copy a step (profiles/r04p_venv_pieces.txt).)
     """
 
     metadata = {"render_modes": [], "render_fps": 60}
@@ -227,13 +235,15 @@ class FootsiesVectorEnv(_VectorEnvBase):
 
     def __init__(self, num_envs, device=0, opponent=None, dense_reward=True, frame_delay=0,
                  autoreset_mode="same_step", float_mode="strict", seed=0, vs_player=False, by_example=False,
-                 output="numpy", _host_outputs=False):
+                 output="numpy", _host_outputs=None):
         if vs_player:
             raise ValueError("vs_player needs a human at the game window; not available in the simulator")
         if not 0 <= int(frame_delay) <= _abi.FS_MAX_FRAME_DELAY:
             raise ValueError("frame_delay must be in [0, %d]" % _abi.FS_MAX_FRAME_DELAY)
         if output not in ("numpy", "torch"):
             raise ValueError("output must be 'numpy' or 'torch'")
+        if _host_outputs is None:
+            _host_outputs = output == "numpy"
         if _host_outputs and output != "numpy":
             raise ValueError("host-memory outputs serve the numpy output only")
         self.num_envs = int(num_envs)
