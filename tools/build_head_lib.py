@@ -22,15 +22,18 @@ def main(rev, out):
     with open(os.path.join(inc, "footsies.h"), "wb") as fh:
         fh.write(subprocess.run(["git", "-C", ROOT, "show", "%s:include/footsies.h" % rev], check=True,
                                 capture_output=True).stdout)
+    present = set()
     for f in os.listdir(B.CSRC):
         if f.endswith((".hip", ".cpp", ".h")):
             rel = os.path.relpath(os.path.join(B.CSRC, f), ROOT)
-            data = subprocess.run(["git", "-C", ROOT, "show", "%s:%s" % (rev, rel)], check=True,
-                                  capture_output=True).stdout
+            r = subprocess.run(["git", "-C", ROOT, "show", "%s:%s" % (rev, rel)], capture_output=True)
+            if r.returncode:  # (a file the revision does not have yet)
+                continue
+            present.add(f)
             with open(os.path.join(src, f), "wb") as fh:
-                fh.write(data)
+                fh.write(r.stdout)
     objs = []
-    for s in B.SOURCES:
+    for s in (s for s in B.SOURCES if s in present):
         o = os.path.join(out, s + ".o")
         subprocess.run([B._hipcc(), "--offload-arch=" + B.ARCH, *B.flags_for(s), "-I", inc,
                         "-c", os.path.join(src, s), "-o", o], check=True)
