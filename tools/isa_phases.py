@@ -205,14 +205,20 @@ def main():
         return "other: " + names[-1]
 
     per = collections.defaultdict(collections.Counter)
+    cls = collections.defaultdict(collections.Counter)  # VALU issue classes (tools/issue_model.classify)
+    prev_vcc = False
     for (addr, mn, ops, size), ch in zip(loop, chains):
-        per[phase_of(ch)][kind(mn)] += 1
+        ph = phase_of(ch)
+        per[ph][kind(mn)] += 1
+        if mn.startswith("v_") and not mn.startswith(("v_readfirstlane", "v_readlane", "v_writelane", "v_mfma")):
+            cls[ph][IM.classify(mn, ops, size, prev_vcc)] += 1
+            prev_vcc = IM.reads_vcc(mn, ops)
     ticks = 2  # the main loop is the row loop unrolled by two ticks
     rows, common, rare = [], collections.Counter(), collections.Counter()
     for ph, c in per.items():
         tot = sum(c.values())
         row = {"phase": ph, "per_tick": {k: v / ticks for k, v in sorted(c.items())}, "total_per_tick": tot / ticks,
-               "rare": RARE_TAG in ph}
+               "valu_classes_per_tick": {k: v / ticks for k, v in sorted(cls[ph].items())}, "rare": RARE_TAG in ph}
         rows.append(row)
         (rare if row["rare"] else common).update(c)
     rows.sort(key=lambda r: (r["rare"], -r["per_tick"].get("valu", 0), -r["total_per_tick"]))
@@ -234,9 +240,11 @@ def main():
             res["measured_per_wave_tick"] = {"valu": pw.get("SQ_INSTS_VALU"), "salu": pw.get("SQ_INSTS_SALU"),
                                              "lds": pw.get("SQ_INSTS_LDS"), "source": os.path.relpath(a.sq, ROOT)}
     for r in rows:
-        print("%-82s valu %6.1f  salu %5.1f  lds %4.1f  vmem %4.1f  all %6.1f" % (
+        vc = r["valu_classes_per_tick"]
+        print("%-82s valu %6.1f  salu %5.1f  lds %4.1f  vmem %4.1f  all %6.1f | vopc %4.1f vop3 %5.1f fast %5.1f" % (
             r["phase"][:82], r["per_tick"].get("valu", 0), r["per_tick"].get("salu", 0), r["per_tick"].get("lds", 0),
-            r["per_tick"].get("vmem", 0), r["total_per_tick"]))
+            r["per_tick"].get("vmem", 0), r["total_per_tick"], vc.get("vopc", 0), vc.get("vop3_op", 0),
+            vc.get("fast", 0)))
     print("common path per tick:", res["common_path_per_tick"])
     if a.json:
         with open(a.json, "w") as f:
