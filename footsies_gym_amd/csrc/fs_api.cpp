@@ -129,6 +129,8 @@ void set_p2bot_mirror(fs_context* h, size_t i, uint8_t bot) {
 }
 
 int use_device(fs_context* h) {
+  int cur = -1;  // (the calling thread is usually on the handle's device already: no hipSetDevice)
+  if (hipGetDevice(&cur) == hipSuccess && cur == h->device) return FS_OK;
   HIP_TRY(h, hipSetDevice(h->device));
   return FS_OK;
 }
