@@ -327,3 +327,40 @@ def test_native_host_conversion_equals_numpy(n, threads, monkeypatch):
         assert np.array_equal(fi["p2_action"], [bool(out["final_action"][j, 1] & b) for b in (1, 2, 4)])
         assert fi["frame"] == out["final_frame"][j] and fi["p1_hitstun"] == out["final_hitstun"][j, 0]
     assert all(i["final_observation"][j] is None for j in np.nonzero(out["terminated"] == 0)[0][:50])
+
+
+def test_native_conversion_source_cache_follows_the_arrays():
+    """_host_convert caches the fs_outputs struct of the source arrays it last saw (the sim's pinned
+    views repeat every step).  The cache must follow the arrays: new values written in place are
+    read again, and a dict holding other array objects (or a converted copy of a wrong-dtype
+    source, never cached) gets its own struct."""
+    from footsies_gym_amd import vector_env as V
+    rng = np.random.default_rng(3)
+
+    def outputs(n):
+        o = {"guard": rng.integers(0, 4, (n, 2)).astype(np.uint8), "move": rng.integers(0, 17, (n, 2)).astype(np.uint8),
+             "move_frame": rng.integers(0, 60, (n, 2)).astype(np.float32),
+             "position": (rng.standard_normal((n, 2)) * 3).astype(np.float32),
+             "action": rng.integers(0, 8, (n, 2)).astype(np.uint8), "hitstun": rng.integers(0, 30, (n, 2)).astype(np.uint8),
+             "frame": rng.integers(-1, 3000, n).astype(np.int32), "reward": rng.standard_normal(n),
+             "terminated": (rng.random(n) < 0.3).astype(np.uint8), "truncated": np.zeros(n, np.uint8)}
+        return o
+
+    def same(a, b):
+        return all(np.array_equal(a[k], b[k]) for k in b)
+
+    a, b = outputs(300), outputs(300)
+    for out in (a, b, a, a):  # alternating dicts, then the same arrays twice
+        obs, info = V.obs_info_from_outputs(out)
+        eobs, einfo = V.obs_info_from_outputs_numpy(out)
+        assert same(obs, eobs) and same(info, einfo)
+    a["position"][:] = -a["position"]  # new values in the cached arrays
+    a["frame"][:] = 7
+    obs, info = V.obs_info_from_outputs(a)
+    assert np.array_equal(obs["position"], a["position"])
+    assert (info["frame"] == 7).all()
+    c = dict(a, frame=a["frame"].astype(np.int64))  # a wrong-dtype source: converted, not cached
+    obs, info = V.obs_info_from_outputs(c)
+    assert (info["frame"] == 7).all() and info["frame"].dtype == np.int64
+    a["frame"][:] = 9
+    assert (V.obs_info_from_outputs(a)[1]["frame"] == 9).all()
