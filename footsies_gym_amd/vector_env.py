@@ -122,18 +122,26 @@ def _src_struct(out, prefix, want_step):
     return so, keep
 
 
-def _host_convert(out, prefix, rows, n, want_step):
+_DST_NO_COPIES = tuple(m for m in _DST_ROWS[:13] if not m[0].startswith("info_"))
+
+
+def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
     """(obs, info[, (reward, terminated, truncated)]) of n rows of host outputs through
-    fs_host_convert (one pass over the rows on the library's host threads)."""
+    fs_host_convert (one pass over the rows on the library's host threads).  info_copies=False:
+    the info gets no observation entries (the caller shares the obs rows, see
+    step_result_from_outputs)."""
     so, keep = _src_struct(out, prefix, want_step)
-    members = _DST_ROWS if want_step else _DST_ROWS[:13]
+    members = _DST_ROWS if want_step else (_DST_ROWS[:13] if info_copies else _DST_NO_COPIES)
     offs, total = [], 0
     for m in members:  # 64-B aligned members of one block
         offs.append(total)
         total += (n * m[3] + 63) & ~63
     block = np.empty(total or 1, np.uint8)
     base = block.ctypes.data
-    dst = _abi.fs_host_arrays(*[base + off for off in offs])
+    if info_copies:
+        dst = _abi.fs_host_arrays(*[base + off for off in offs])
+    else:  # (the info_ members stay null: fs_host_convert skips them)
+        dst = _abi.fs_host_arrays(**{m[0]: base + off for m, off in zip(members, offs)})
     views = {name: np.ndarray((n, c) if c else (n,), dt, block, off)
              for (name, dt, c, _), off in zip(members, offs)}
     r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
@@ -142,7 +150,8 @@ def _host_convert(out, prefix, rows, n, want_step):
     del keep  # (the converted sources lived over the call)
     obs = {k: views[k] for k in ("guard", "move", "move_frame", "position")}
     info = {k: views[k] for k in ("frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun")}
-    info.update({k: views["info_" + k] for k in ("guard", "move", "move_frame", "position")})  # FE:379's copies
+    if info_copies:
+        info.update({k: views["info_" + k] for k in ("guard", "move", "move_frame", "position")})  # FE:379's copies
     extra = (views["reward"], views["terminated"], views["truncated"]) if want_step else None
     return obs, info, extra
 
@@ -186,19 +195,20 @@ def step_result_from_outputs(out, autoreset_mode="same_step"):
     if autoreset_mode == "same_step" and term.any():
         idx = np.nonzero(term)[0]
         # only the terminated arenas' final outputs are converted
-        fobs, finfo, _ = _host_convert(out, "final_", idx, len(idx), False)
+        fobs, finfo, _ = _host_convert(out, "final_", idx, len(idx), False, info_copies=False)
         final_obs = np.empty(len(term), dtype=object)
         final_info = np.empty(len(term), dtype=object)
         # Per-arena dicts (gymnasium 0.29's contract: one dict per terminated env, None elsewhere),
         # their values the rows of the batched final arrays: list(a) makes every row view in one C
-        # loop, and literal dicts are built without a zip per entry.
+        # loop, and literal dicts are built without a zip per entry.  An arena's final info holds
+        # the same observation rows as its final observation, as FE:379's `**obs` puts the obs
+        # dict's own values (tuples) into the reference's info.
         g, m, mf, pos = (list(fobs[k]) for k in ("guard", "move", "move_frame", "position"))
         final_obs[idx] = [{"guard": a, "move": b, "move_frame": c, "position": d} for a, b, c, d in zip(g, m, mf, pos)]
-        fr, a1, a2, h1, h2, ig, im, imf, ipos = (list(finfo[k]) for k in (
-            "frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun", "guard", "move", "move_frame", "position"))
+        fr, a1, a2, h1, h2 = (list(finfo[k]) for k in ("frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun"))
         final_info[idx] = [{"frame": v0, "p1_action": v1, "p2_action": v2, "p1_hitstun": v3, "p2_hitstun": v4,
                             "guard": v5, "move": v6, "move_frame": v7, "position": v8}
-                           for v0, v1, v2, v3, v4, v5, v6, v7, v8 in zip(fr, a1, a2, h1, h2, ig, im, imf, ipos)]
+                           for v0, v1, v2, v3, v4, v5, v6, v7, v8 in zip(fr, a1, a2, h1, h2, g, m, mf, pos)]
         info["final_observation"] = final_obs
         info["_final_observation"] = term.copy()
         info["final_info"] = final_info

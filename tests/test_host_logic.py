@@ -326,6 +326,10 @@ def test_native_host_conversion_equals_numpy(n, threads, monkeypatch):
         assert np.array_equal(fo["guard"], out["final_guard"][j].astype(np.int64))
         assert np.array_equal(fi["p2_action"], [bool(out["final_action"][j, 1] & b) for b in (1, 2, 4)])
         assert fi["frame"] == out["final_frame"][j] and fi["p1_hitstun"] == out["final_hitstun"][j, 0]
+        # the final info's observation entries are the final observation's own rows (FE:379's **obs)
+        assert list(fi) == ["frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun", "guard", "move",
+                            "move_frame", "position"]
+        assert all(fi[k] is fo[k] for k in fo)
     assert all(i["final_observation"][j] is None for j in np.nonzero(out["terminated"] == 0)[0][:50])
 
 

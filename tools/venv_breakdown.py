@@ -77,19 +77,18 @@ def pieces_of(out):
     t = _tick("main convert", t)
     idx = np.nonzero(term)[0]
     t = _tick("nonzero", t)
-    fobs, finfo, _ = ve._host_convert(out, "final_", idx, len(idx), False)
+    fobs, finfo, _ = ve._host_convert(out, "final_", idx, len(idx), False, info_copies=False)
     t = _tick("final convert", t)
     final_obs = np.empty(len(term), dtype=object)
     final_info = np.empty(len(term), dtype=object)
     t = _tick("object arrays", t)
     g, m, mf, pos = (list(fobs[k]) for k in ("guard", "move", "move_frame", "position"))
-    fr, a1, a2, h1, h2, ig, im, imf, ipos = (list(finfo[k]) for k in (
-        "frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun", "guard", "move", "move_frame", "position"))
+    fr, a1, a2, h1, h2 = (list(finfo[k]) for k in ("frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun"))
     t = _tick("row views", t)
     final_obs[idx] = [{"guard": a, "move": b, "move_frame": c, "position": d} for a, b, c, d in zip(g, m, mf, pos)]
     final_info[idx] = [{"frame": v0, "p1_action": v1, "p2_action": v2, "p1_hitstun": v3, "p2_hitstun": v4,
                         "guard": v5, "move": v6, "move_frame": v7, "position": v8}
-                       for v0, v1, v2, v3, v4, v5, v6, v7, v8 in zip(fr, a1, a2, h1, h2, ig, im, imf, ipos)]
+                       for v0, v1, v2, v3, v4, v5, v6, v7, v8 in zip(fr, a1, a2, h1, h2, g, m, mf, pos)]
     t = _tick("dicts", t)
     info["final_observation"] = final_obs
     info["_final_observation"] = term.copy()
