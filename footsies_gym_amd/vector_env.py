@@ -123,6 +123,10 @@ def _src_struct(out, prefix, want_step):
 
 
 _DST_NO_COPIES = tuple(m for m in _DST_ROWS[:13] if not m[0].startswith("info_"))
+# The destination members live in three blocks, one allocation each: the observation, the info and
+# the step's (reward, terminated, truncated).  A caller that keeps one of a step's arrays (a rollout
+# that appends `terminated`) holds only that array's block alive, not all ~9 MB of the step.
+_BLOCK_OF = {"guard": 0, "move": 0, "move_frame": 0, "position": 0, "reward": 2, "terminated": 2, "truncated": 2}
 
 
 def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
@@ -132,18 +136,19 @@ def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
     step_result_from_outputs)."""
     so, keep = _src_struct(out, prefix, want_step)
     members = _DST_ROWS if want_step else (_DST_ROWS[:13] if info_copies else _DST_NO_COPIES)
-    offs, total = [], 0
-    for m in members:  # 64-B aligned members of one block
-        offs.append(total)
-        total += (n * m[3] + 63) & ~63
-    block = np.empty(total or 1, np.uint8)
-    base = block.ctypes.data
+    offs, totals = [], [0, 0, 0]
+    for m in members:  # 64-B aligned members of their block
+        b = _BLOCK_OF.get(m[0], 1)
+        offs.append((b, totals[b]))
+        totals[b] += (n * m[3] + 63) & ~63
+    blocks = [np.empty(t or 1, np.uint8) for t in totals]
+    bases = [blk.ctypes.data for blk in blocks]
     if info_copies:
-        dst = _abi.fs_host_arrays(*[base + off for off in offs])
+        dst = _abi.fs_host_arrays(*[bases[b] + off for b, off in offs])
     else:  # (the info_ members stay null: fs_host_convert skips them)
-        dst = _abi.fs_host_arrays(**{m[0]: base + off for m, off in zip(members, offs)})
-    views = {name: np.ndarray((n, c) if c else (n,), dt, block, off)
-             for (name, dt, c, _), off in zip(members, offs)}
+        dst = _abi.fs_host_arrays(**{m[0]: bases[b] + off for m, (b, off) in zip(members, offs)})
+    views = {name: np.ndarray((n, c) if c else (n,), dt, blocks[b], off)
+             for (name, dt, c, _), (b, off) in zip(members, offs)}
     r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
     check(lib().fs_host_convert(C.byref(so), None if r is None else r.ctypes.data, n, C.byref(dst),
                                 host_threads()))
