@@ -123,10 +123,11 @@ def _src_struct(out, prefix, want_step):
 
 
 _DST_NO_COPIES = tuple(m for m in _DST_ROWS[:13] if not m[0].startswith("info_"))
-# The destination members live in three blocks, one allocation each: the observation, the info and
-# the step's (reward, terminated, truncated).  A caller that keeps one of a step's arrays (a rollout
-# that appends `terminated`) holds only that array's block alive, not all ~9 MB of the step.
-_BLOCK_OF = {"guard": 0, "move": 0, "move_frame": 0, "position": 0, "reward": 2, "terminated": 2, "truncated": 2}
+# The destination members live in five blocks, one allocation each: the observation, the info,
+# and the reward, terminated and truncated arrays on their own.  A caller that keeps one of a step's
+# arrays (a rollout that appends `terminated`) holds only that array's block alive, not all ~9 MB of
+# the step, whose blocks the next step then reuses.
+_BLOCK_OF = {"guard": 0, "move": 0, "move_frame": 0, "position": 0, "reward": 2, "terminated": 3, "truncated": 4}
 
 
 def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
@@ -136,12 +137,12 @@ def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
     step_result_from_outputs)."""
     so, keep = _src_struct(out, prefix, want_step)
     members = _DST_ROWS if want_step else (_DST_ROWS[:13] if info_copies else _DST_NO_COPIES)
-    offs, totals = [], [0, 0, 0]
+    offs, totals = [], [0, 0, 0, 0, 0]
     for m in members:  # 64-B aligned members of their block
         b = _BLOCK_OF.get(m[0], 1)
         offs.append((b, totals[b]))
         totals[b] += (n * m[3] + 63) & ~63
-    blocks = [np.empty(t or 1, np.uint8) for t in totals]
+    blocks = [np.empty(t or 1, np.uint8) for t in (totals if want_step else totals[:2])]
     bases = [blk.ctypes.data for blk in blocks]
     if info_copies:
         dst = _abi.fs_host_arrays(*[bases[b] + off for b, off in offs])

@@ -319,6 +319,9 @@ def test_native_host_conversion_equals_numpy(n, threads, monkeypatch):
     assert all(info[k] is not obs[k] and not np.shares_memory(info[k], obs[k]) for k in obs)
     o, r, t, tr, i = V.step_result_from_outputs(out)
     assert r.dtype == np.float64 and np.array_equal(r, out["reward"]) and t.dtype == np.bool_
+    # observation, info, reward, terminated and truncated sit in separate allocations: keeping one
+    # (a rollout appending `terminated`) does not keep the step's other arrays alive
+    assert len({id(x.base) for x in (o["guard"], i["frame"], r, t, tr)}) == 5
     assert np.array_equal(t, out["terminated"] != 0) and not tr.any()
     idx = np.nonzero(out["terminated"])[0]
     for j in idx[:50]:
