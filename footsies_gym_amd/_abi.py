@@ -6,7 +6,7 @@ the test-side oracle binding (``oracle/binding.py``) agree on layouts.
 """
 import ctypes as C
 
-FS_ABI_VERSION = 3
+FS_ABI_VERSION = 4
 
 FS_OK = 0
 FS_E_INVALID = -1
@@ -39,6 +39,8 @@ FS_MAX_FRAME_DELAY = 4096
 FS_RECORD_BYTES = 40
 FS_KERNEL_HASHED = 1
 FS_KERNEL_POLICY = 2
+FS_KERNEL_PACKED = 4
+FS_PACKED_LANE_BYTES = 16
 FS_PPO_ACTOR_PARAMS = 5256
 FS_PPO_CRITIC_PARAMS = 4801
 FS_PPO_FP32 = 0
@@ -99,6 +101,10 @@ class fs_host_arrays(C.Structure):
         "frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun", "reward", "terminated", "truncated")]
 
 
+class fs_packed_traj(C.Structure):
+    _fields_ = [("lanes", C.c_void_p), ("reward", C.c_void_p), ("final_lanes", C.c_void_p)]
+
+
 class fs_policy(C.Structure):
     _fields_ = [
         ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p), ("w3", C.c_void_p),
@@ -155,6 +161,7 @@ LIB_FUNCTIONS = {
     "fs_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_masked": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_step_n": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(fs_outputs)]),
+    "fs_step_n_packed": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(fs_packed_traj)]),
     "fs_step_n_policy": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(fs_policy), C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_ppo_workspace_bytes": (C.c_size_t, []),
     "fs_ppo_eval": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp),

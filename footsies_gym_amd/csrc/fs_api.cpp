@@ -311,7 +311,7 @@ FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int
 
 static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2, int flags, uint64_t seed,
                        const fs_outputs* traj, const uint8_t* active = nullptr,
-                       const fs_policy* pol = nullptr) {
+                       const fs_policy* pol = nullptr, const fs_packed_traj* pk = nullptr) {
   int rc;
   if ((rc = use_device(h))) return rc;
   const size_t N = (size_t)h->n;
@@ -382,6 +382,12 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
          !traj->final_frame || !traj->final_action || !traj->final_hitstun))
       return set_err(h, FS_E_INVALID, "fs_step_n: final_* trajectory buffers required in same-step autoreset");
     sp.out_stride_steps = 1;
+  } else if (pk) {  // (fs_step_n_packed validated the buffers)
+    sp.out = fsk::DevOutputs{};
+    sp.out.reward = pk->reward;
+    sp.out.pk_lanes = static_cast<uint4*>(pk->lanes);
+    sp.out.pk_final = static_cast<uint4*>(pk->final_lanes);
+    sp.out_stride_steps = 1;
   } else if (n > 1 && h->cfg.frame_delay > 0) {
     // the delayed queue needs every step's row, which a fused launch without a
     // trajectory overwrites: step one tick per launch instead
@@ -405,15 +411,17 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
 // of the same buffers.  Hashed actions and the actor's sampling stream are keyed by the
 // handle's step counter, which each launch advances, so the split is invisible in the results.
 constexpr uint64_t kMaxLaunchRows = 0xFFFFFFFFull / 8u;
+// (a packed trajectory's lane records: 32 B per row)
+constexpr uint64_t kMaxPackedLaunchRows = 0xFFFFFFFFull / 32u;
 
 static int step_chunked(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2, uint64_t seed,
-                        const fs_outputs* traj, const fs_policy* pol) {
+                        const fs_outputs* traj, const fs_policy* pol, const fs_packed_traj* pk = nullptr) {
   const uint64_t N = (uint64_t)h->n;
-  uint64_t rows = kMaxLaunchRows;
+  uint64_t rows = pk ? kMaxPackedLaunchRows : kMaxLaunchRows;
   if (const char* e = getenv("FOOTSIES_MAX_LAUNCH_ROWS"))  // test hook: exercise the split at small sizes
     rows = std::min<uint64_t>(rows, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
   const int max_n = (int)std::max<uint64_t>(1, std::min<uint64_t>(rows / N, 0x7fffffff));
-  if (n <= max_n) return step_common(h, n, p1, p2, FS_ACT_DEVICE, seed, traj, nullptr, pol);
+  if (n <= max_n) return step_common(h, n, p1, p2, FS_ACT_DEVICE, seed, traj, nullptr, pol, pk);
   for (int j = 0; j < n;) {
     const int m = std::min(max_n, n - j);
     const uint64_t row = (uint64_t)j * N;  // first arena-tick row of this launch
@@ -432,8 +440,15 @@ static int step_chunked(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2
       if (q.actions_out) q.actions_out += row;
       if (q.logp_out) q.logp_out += row;
     }
+    fs_packed_traj k{};
+    if (pk) {
+      k = *pk;
+      k.lanes = static_cast<char*>(k.lanes) + row * 2 * FS_PACKED_LANE_BYTES;
+      k.reward += row;
+      if (k.final_lanes) k.final_lanes = static_cast<char*>(k.final_lanes) + row * 2 * FS_PACKED_LANE_BYTES;
+    }
     const int rc = step_common(h, m, p1 ? p1 + row : nullptr, p2 ? p2 + row : nullptr, FS_ACT_DEVICE, seed,
-                               traj ? &t : nullptr, nullptr, pol ? &q : nullptr);
+                               traj ? &t : nullptr, nullptr, pol ? &q : nullptr, pk ? &k : nullptr);
     if (rc) return rc;
     j += m;
   }
@@ -492,6 +507,26 @@ FS_API int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p
       !(p1_act == nullptr && h->cfg.p1_mode == FS_P1_BOT))
     return set_err(h, FS_E_INVALID, "fs_step_n: give both action arrays or neither");
   return step_chunked(h, n, p1_act, p2_act, action_seed, traj, nullptr);
+}
+
+FS_API int fs_step_n_packed(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act,
+                            const fs_packed_traj* traj) {
+  if (!h) return FS_E_INVALID;
+  if (n <= 0) return set_err(h, FS_E_INVALID, "fs_step_n_packed: n must be > 0");
+  if (!p1_act) return set_err(h, FS_E_INVALID, "fs_step_n_packed: p1 action rows required");
+  if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
+    return set_err(h, FS_E_INVALID, "fs_step_n_packed: p2 action rows required for FS_P2_EXTERNAL");
+  if (!traj || !traj->lanes || !traj->reward)
+    return set_err(h, FS_E_INVALID, "fs_step_n_packed: lanes and reward buffers required");
+  if (h->cfg.autoreset_mode == FS_AUTORESET_SAME_STEP && !traj->final_lanes)
+    return set_err(h, FS_E_INVALID, "fs_step_n_packed: final_lanes required in same-step autoreset");
+  if (reinterpret_cast<uintptr_t>(traj->lanes) % 16 || reinterpret_cast<uintptr_t>(traj->final_lanes) % 16 ||
+      reinterpret_cast<uintptr_t>(traj->reward) % 8)
+    return set_err(h, FS_E_INVALID, "fs_step_n_packed: lanes / final_lanes must be 16-byte, reward 8-byte aligned");
+  if (h->cfg.frame_delay > 0)
+    return set_err(h, FS_E_UNSUPPORTED, "fs_step_n_packed: frame_delay > 0 is not supported (the delayed queue "
+                                        "reads the per-field outputs)");
+  return step_chunked(h, n, p1_act, p2_act, 0, nullptr, nullptr, traj);
 }
 
 FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint8_t* p2_act,
@@ -777,9 +812,9 @@ FS_API int fs_set_stream(fs_handle h, void* stream) {
 }
 
 FS_API const char* fs_step_kernel(fs_handle h, int n_steps, int flags) {
-  if (!h || n_steps <= 0 || (flags & ~(FS_KERNEL_HASHED | FS_KERNEL_POLICY))) return nullptr;
+  if (!h || n_steps <= 0 || (flags & ~(FS_KERNEL_HASHED | FS_KERNEL_POLICY | FS_KERNEL_PACKED))) return nullptr;
   return fsk::step_kernel_name((flags & FS_KERNEL_POLICY) != 0, (flags & FS_KERNEL_HASHED) != 0, n_steps, h->n,
-                               h->cfg.float_mode, variant(h), h->geom);
+                               h->cfg.float_mode, variant(h), h->geom, (flags & FS_KERNEL_PACKED) != 0);
 }
 
 FS_API int fs_num_envs(fs_handle h) { return h ? h->n : 0; }

@@ -58,6 +58,10 @@ struct DevOutputs {
   int32_t* final_frame;
   uint8_t* final_action;
   uint8_t* final_hitstun;
+  // fs_step_n_packed (include/footsies.h fs_packed_traj): lane records of 16 B, with `reward`
+  // above as the trajectory's reward; the per-field pointers are then unused
+  uint4* pk_lanes;
+  uint4* pk_final;
 };
 
 // the in-kernel actor of fs_step_n_policy (fs_policy.h): fp32 weights in torch layouts
@@ -129,7 +133,7 @@ struct DelayParams {
 // variant: FS_P2_EXTERNAL / FS_P2_BOT / FS_P2_NOOP or kActors (see above)
 hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStream_t s);
 const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant,
-                             bool geom);
+                             bool geom, bool packed);
 hipError_t launch_reset(const ResetParams& p, int float_mode, hipStream_t s);
 hipError_t launch_set_p2(const DevState& st, int bot, const uint8_t* mask, int n, hipStream_t s);
 hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint64_t arena_base, uint8_t* p1,

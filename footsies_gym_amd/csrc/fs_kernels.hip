@@ -1295,6 +1295,28 @@ __device__ __forceinline__ void write_final(const Lane& L, const DevOutputs& o, 
             o.final_hitstun, r);
 }
 
+// fs_step_n_packed (include/footsies.h fs_packed_traj): the values write_obs stores, as one 16-B
+// record per lane -- the guard / move / action / hitstun bytes, move_frame, position and a fourth
+// word w3 (P1: the frame; P2: the terminated / truncated bytes) -- so that a tick's outputs take
+// two store instructions (this record and the f64 reward) instead of ten.
+typedef uint32_t PkRec __attribute__((ext_vector_type(4)));  // a native vector: one 16-B store
+__device__ __forceinline__ PkRec packed_record(const Lane& L, uint32_t w3) {
+  int a = L.f.act;
+  if (a == A_DEAD || a == A_WIN) a = A_STAND;  // FE:537-549
+  const int mf = (a == A_STAND || a == A_FORWARD || a == A_BACKWARD) ? 0 : L.f.frame;  // FE:339-358
+  const uint32_t act = L.rec_count > 0 ? (uint32_t)L.rec & 0xffu : 0u;
+  PkRec v;
+  v.x = ((uint32_t)L.f.guard & 0xffu) | (((uint32_t)a & 0xffu) << 8) | (act << 16) | (((uint32_t)L.f.stun & 0xffu) << 24);
+  v.y = __float_as_uint((float)mf);
+  v.z = __float_as_uint(L.f.x);
+  v.w = w3;
+  return v;
+}
+// lane record c = 2 r + k of row r (byte offset 16 c: the host keeps 32 r below 2^32)
+__device__ __forceinline__ void write_packed(const Lane& L, uint4* base, uint32_t r, uint32_t w3) {
+  st_off(reinterpret_cast<PkRec*>(base), 16u * (2u * r + L.k), packed_record(L, w3));
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1322,7 +1344,7 @@ __device__ __forceinline__ uint32_t hash_action(uint64_t seed, uint64_t env, uin
 // tick t's stores the wave waits with vmcnt(11): at least 11 vector memory ops were issued after
 // that load -- tick t-1's output stores (10 on every path of env_step: write_main's 7 plus reward,
 // terminated, truncated) and tick t+2's load -- so the row is resident while those stores may
-// still be in flight.  The loaded register is read by nothing but the wait statement, which copies
+// still be in flight.  (Packed trajectories, PK: 2 stores per tick, so vmcnt(3).)  The loaded register is read by nothing but the wait statement, which copies
 // the row out after the s_waitcnt; tools/check_async_loads.py checks on the assembly that no
 // instruction touches a register between its load and its wait, and that on every path at least
 // 11 vector memory instructions are issued between each row load and its wait
@@ -1379,7 +1401,7 @@ __device__ __forceinline__ void opaque_burst_results(Lane& L) {
                "+v"(L.rec_count));
 }
 
-template <int FM, int P2, int WAIT = -1, int TP = kTabLds, bool GEOM = false>
+template <int FM, int P2, int WAIT = -1, int TP = kTabLds, bool GEOM = false, bool PK = false>
 __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   constexpr bool G = TP == kTabGlobal;  // the tables from global memory: a one-tick launch (k_step),
@@ -1398,10 +1420,15 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.cum = 0.0;
     L.ai = stand_info();  // the burst ends on STAND
     settle_w<WAIT>(next);
-    write_main(L, o, r);
-    st_off(o.reward, 8 * r, 0.0);  // per-arena outputs: both lanes store the same value (no divergent branch)
-    st_off(o.terminated, r, (uint8_t)0);
-    st_off(o.truncated, r, (uint8_t)0);
+    if constexpr (PK) {
+      write_packed(L, o.pk_lanes, r, k == 0 ? (uint32_t)L.frame_count : 0u);
+      st_off(o.reward, 8 * r, 0.0);
+    } else {
+      write_main(L, o, r);
+      st_off(o.reward, 8 * r, 0.0);  // per-arena outputs: both lanes store the same value (no divergent branch)
+      st_off(o.terminated, r, (uint8_t)0);
+      st_off(o.truncated, r, (uint8_t)0);
+    }
     opaque_burst_results(L);
     return;
   }
@@ -1502,7 +1529,8 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     L.f.hist = 0;  // ChangeRoundState(KO): ClearInput (BC:296-299)
     L.f.hold = 0;
     if (p.autoreset_mode == FS_AUTORESET_SAME_STEP) {
-      write_final(L, o, r);
+      if constexpr (PK) write_packed(L, o.pk_final, r, k == 0 ? (uint32_t)L.frame_count : 0u);
+      else write_final(L, o, r);
       reset_burst<FM, P2, G>(L, true, ac);
       if constexpr (GEOM) {
         L.f.y = 0.0f;
@@ -1528,10 +1556,15 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     }
     L.has_term = false;
   }
-  write_main(L, o, r);
-  st_off(o.reward, 8 * r, reward);  // identical on both lanes of the arena
-  st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
-  st_off(o.truncated, r, (uint8_t)0);
+  if constexpr (PK) {
+    write_packed(L, o.pk_lanes, r, k == 0 ? (uint32_t)L.frame_count : (over ? 1u : 0u));
+    st_off(o.reward, 8 * r, reward);  // identical on both lanes of the arena
+  } else {
+    write_main(L, o, r);
+    st_off(o.reward, 8 * r, reward);  // identical on both lanes of the arena
+    st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
+    st_off(o.truncated, r, (uint8_t)0);
+  }
   // all four words live until here (the tick reads three; see R.push above)
   if constexpr (!G) asm volatile("" ::"v"(L.ai));
 }
@@ -1553,8 +1586,9 @@ __device__ __forceinline__ void policy_features(const Lane& L, uint32_t& d0, uin
 // POL samples P1's action every tick from the MLP actor (fs_policy.h); its MFMAs and lane
 // exchanges need the whole wave, so lanes past the last arena stay in the loop (on a copy
 // of arena 0 that they never store) unless their whole wave is idle.
-template <int FM, int P2, bool FUSED, bool HASH, bool POL = false, bool GEOM = false>
+template <int FM, int P2, bool FUSED, bool HASH, bool POL = false, bool GEOM = false, bool PK = false>
 __device__ __forceinline__ void step_body(const StepParams& p) {
+  static_assert(!PK || (FUSED && !HASH && !POL), "packed trajectories: the fused row loop only");
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = l < 2 * p.n_envs;
   const int a = active ? l >> 1 : 0;
@@ -1642,6 +1676,9 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       // issued every tick (the last rows re-read the last one) so the wait counts hold, and the
       // last one in flight is waited for before the wave ends.  (Rows 0 and 1 were issued before
       // the table staging.)
+      // (the wait count of settle_w: the vector memory ops every path issues between a row's load
+      // and its wait -- one tick's output stores, 10 per-field or 2 packed, plus the next row load)
+      constexpr int kRowWait = PK ? 3 : 11;
       uint32_t a_fl = next, b_fl = row1, a_rd, b_rd;
       asm volatile("s_waitcnt vmcnt(0)\n\tv_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(a_rd), "=v"(b_rd)
                    : "v"(a_fl), "v"(b_fl) : "memory");
@@ -1650,19 +1687,19 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       for (; t < last; t += 2) {
         a_fl = issue(t + 2);
         if (p.prio) prio_slice(grp);
-        env_step<FM, P2, 11, kTabLds, GEOM>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
+        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
         b_rd = b_fl;
         b_fl = issue(t + 3);
         if (p.prio) prio_slice(grp);
-        env_step<FM, P2, 11, kTabLds, GEOM>(L, reads ? b_rd & 7u : 0u, p, (uint32_t)(t + 1) * row_step + (uint32_t)a,
-                                            a_fl);
+        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK>(L, reads ? b_rd & 7u : 0u, p,
+                                                (uint32_t)(t + 1) * row_step + (uint32_t)a, a_fl);
         a_rd = a_fl;
       }
       if (t == last) {  // an odd tick count: the last tick waits for a re-read of the last row
         a_fl = issue(t + 2);
         uint32_t b_last = b_fl;  // (b_fl itself stays the in-flight value for the final wait)
-        env_step<FM, P2, 11, kTabLds, GEOM>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a,
-                                            b_last);
+        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a,
+                                                b_last);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::"v"(a_fl), "v"(b_fl) : "memory");  // no load outlives the wave
     }
@@ -1752,6 +1789,13 @@ template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n(StepParams p) {
   if (p.geom) step_body<FM, P2, true, false, false, true>(p);
   else step_body<FM, P2, true, false>(p);
+}
+
+// fs_step_n_packed: the row loop of k_step_n storing packed trajectory records
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step_n_packed(StepParams p) {
+  if (p.geom) step_body<FM, P2, true, false, false, true, true>(p);
+  else step_body<FM, P2, true, false, false, false, true>(p);
 }
 
 template <int FM, int P2>
@@ -2069,6 +2113,7 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   StepParams p = p_in;
   p.prio = two_waves_per_simd(p.n_envs);
   if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
+  else if (p.out.pk_lanes) hipLaunchKernelGGL((k_step_n_packed<FM, P2>), grid, block, 0, s, p);  // (rows: fs_api checks)
   else if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
   else if constexpr (P2 != kActors) {
@@ -2097,9 +2142,10 @@ hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStre
 }
 
 // The kernel launch_step_p2 runs for a launch of this shape, as rocprofv3 names it (fs_step_kernel).
-const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant, bool geom) {
+const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant, bool geom,
+                             bool packed) {
   static thread_local char buf[64];
-  const char* k = policy ? "k_step_n_policy" : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step"
+  const char* k = policy ? "k_step_n_policy" : packed ? "k_step_n_packed" : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step"
                 : (variant != kActors && !geom && fused_one_lane(n_envs)) ? "k_step_n1" : "k_step_n";
   snprintf(buf, sizeof buf, "fsk::%s<%d, %d>", k, float_mode == FS_FLOAT_DOUBLE ? 1 : 0, variant);
   return buf;

@@ -227,6 +227,31 @@ class FootsiesSim:
                                     C.c_void_p(q2.data_ptr()) if p2 else None), self._h)
         return p1, q2
 
+    def alloc_packed_trajectory(self, n):
+        """Device buffers for step_n_packed: {"lanes": uint8 [n][N][2][16], "reward": float64
+        [n][N], "final_lanes": uint8 [n][N][2][16] (same-step auto-reset only, else None)}
+        (include/footsies.h fs_packed_traj); unpack_trajectory gives their per-field views."""
+        torch = _torch()
+        shape = (n, self.num_envs, 2, _abi.FS_PACKED_LANE_BYTES)
+        same = self.autoreset_mode == "same_step"
+        return {"lanes": torch.zeros(shape, dtype=torch.uint8, device=self.device),
+                "reward": torch.zeros((n, self.num_envs), dtype=torch.float64, device=self.device),
+                "final_lanes": torch.zeros(shape, dtype=torch.uint8, device=self.device) if same else None}
+
+    def step_n_packed(self, n, p1, p2=None, trajectory=None):
+        """step_n with device action rows p1 / p2 (uint8 [n][N]) into a packed trajectory
+        (fs_step_n_packed: two stores per tick instead of ten; alloc_packed_trajectory)."""
+        traj = trajectory if trajectory is not None else self.alloc_packed_trajectory(n)
+        for name, t in traj.items():
+            if t is not None and (not t.is_contiguous() or t.device != self.device or t.shape[0] < n):
+                raise ValueError("packed trajectory buffer %r: contiguous, on %s, >= %d rows" % (name, self.device, n))
+        fl = traj.get("final_lanes")
+        t = _abi.fs_packed_traj(lanes=traj["lanes"].data_ptr(), reward=traj["reward"].data_ptr(),
+                                final_lanes=None if fl is None else fl.data_ptr())
+        check(lib().fs_step_n_packed(self._h, int(n), C.c_void_p(p1.data_ptr()),
+                                     None if p2 is None else C.c_void_p(p2.data_ptr()), C.byref(t)), self._h)
+        return traj
+
     def alloc_trajectory(self, n):
         torch = _torch()
         out = {}
@@ -326,6 +351,34 @@ def _host(a):
     if isinstance(a, torch.Tensor):
         return a.detach().cpu().numpy()
     return a
+
+
+def unpack_trajectory(traj):
+    """The per-field views (alloc_trajectory's names, dtypes and shapes) of a packed trajectory
+    (FootsiesSim.alloc_packed_trajectory; torch tensors or numpy arrays): strided views, no copy.
+    final_* appear when the trajectory has final_lanes."""
+    is_np = isinstance(traj["lanes"], np.ndarray)
+
+    def typed(buf, kind):  # the 16-B records as 4 words of one type
+        if is_np:
+            return buf.view({"u8": np.uint8, "f32": np.float32, "i32": np.int32}[kind])
+        torch = _torch()
+        return buf.view({"u8": torch.uint8, "f32": torch.float32, "i32": torch.int32}[kind])
+
+    out = {}
+    for pre, key in (("", "lanes"), ("final_", "final_lanes")):
+        buf = traj.get(key)
+        if buf is None:
+            continue
+        b, f, i = typed(buf, "u8"), typed(buf, "f32"), typed(buf, "i32")
+        out[pre + "guard"], out[pre + "move"] = b[..., 0], b[..., 1]
+        out[pre + "action"], out[pre + "hitstun"] = b[..., 2], b[..., 3]
+        out[pre + "move_frame"], out[pre + "position"] = f[..., 1], f[..., 2]
+        out[pre + "frame"] = i[..., 0, 3]
+        if not pre:
+            out["terminated"], out["truncated"] = b[..., 1, 12], b[..., 1, 13]
+    out["reward"] = traj["reward"]
+    return out
 
 
 def _fast_actions(t, dev_index, n):

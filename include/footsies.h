@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 3
+#define FS_ABI_VERSION 4
 
 /* error codes */
 #define FS_OK 0
@@ -258,6 +258,28 @@ int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, co
 int fs_step_n(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act,
               uint64_t action_seed, const fs_outputs* traj);
 
+/* A packed trajectory for fs_step_n_packed: the values of an fs_outputs trajectory in two
+ * stores per tick instead of ten.  Row r = t * N + i (tick t, arena i); k = 0 (P1), 1 (P2):
+ *   lanes[r][k]: 16 bytes -- byte 0 guard, 1 move, 2 action (3-bit MostRecentAction), 3 hitstun;
+ *                bytes 4-7 move_frame (float), 8-11 position (float); bytes 12-15: for k = 0 the
+ *                frame (int32), for k = 1 byte 12 terminated, byte 13 truncated, bytes 14-15 zero.
+ *   reward[r]:   float64, as fs_outputs.reward.
+ *   final_lanes[r][k] (FS_AUTORESET_SAME_STEP; rows of arenas that did not end are left
+ *                untouched): the terminal record in the lanes layout, bytes 12-15 of k = 0 the
+ *                final frame, of k = 1 zero.
+ * lanes and final_lanes must be 16-byte aligned.  Every field equals the corresponding
+ * fs_outputs trajectory field of fs_step_n on the same state and actions. */
+#define FS_PACKED_LANE_BYTES 16
+typedef struct fs_packed_traj {
+  void* lanes;        /* [n][N][2][16 B] */
+  double* reward;     /* [n][N] */
+  void* final_lanes;  /* [n][N][2][16 B]; required in FS_AUTORESET_SAME_STEP */
+} fs_packed_traj;
+
+/* fs_step_n with action rows (p1_act required; p2_act as for fs_step_n) into a packed trajectory.
+ * FS_E_UNSUPPORTED with frame_delay > 0. */
+int fs_step_n_packed(fs_handle h, int n, const uint8_t* p1_act, const uint8_t* p2_act, const fs_packed_traj* traj);
+
 /* The actor of fs_step_n_policy: an MLP 8 -> 64 -> tanh -> 64 -> tanh -> 8 on
  * P1's observation features [guard/3, move/16, move_frame/55, position/4.6] of
  * P1 then P2 (footsies_gym_amd/rollout.py obs_features), fp32 device weights in
@@ -429,10 +451,11 @@ uint64_t fs_steps_taken(fs_handle h);
  * n_steps = 1 is fs_step / fs_step_masked, n_steps > 1 fs_step_n with action rows (its launches
  * pick the one-lane kernel from 2 x 64 x SIMD-count arenas on, FOOTSIES_FUSED_LANES forces
  * either); flags FS_KERNEL_HASHED = fs_step_n without action rows, FS_KERNEL_POLICY =
- * fs_step_n_policy.  For naming profiles and roofline lines; NULL for a bad handle or flags.
+ * fs_step_n_policy, FS_KERNEL_PACKED = fs_step_n_packed.  For naming profiles and roofline lines; NULL for a bad handle or flags.
  * The string stays valid until the calling thread's next call. */
 #define FS_KERNEL_HASHED 1
 #define FS_KERNEL_POLICY 2
+#define FS_KERNEL_PACKED 4  /* fs_step_n_packed */
 const char* fs_step_kernel(fs_handle h, int n_steps, int flags);
 void fs_destroy(fs_handle h);
 /* Last error message of h (or of the last failed fs_create when h is NULL). */

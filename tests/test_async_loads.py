@@ -13,18 +13,22 @@ def test_no_register_touched_while_its_row_is_in_flight():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_async_loads.py")], capture_output=True,
                        text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " 0 findings" in r.stdout and "14 kernels" in r.stdout, r.stdout
+    # k_step_n (8 instances: 2 float modes x 4 P2 variants) and k_step_n_packed (8) read rows, and
+    # k_step_n1 (6: no kActors variant)
+    assert " 0 findings" in r.stdout and "22 kernels" in r.stdout, r.stdout
 
 
 def test_wait_counts_are_proven_and_a_too_deep_wait_is_caught(tmp_path):
-    """The same analysis proves every `s_waitcnt vmcnt(11)` row wait: on every path at least 11
-    vector memory instructions follow the row's load (advisor r02).  A copy of the kernel whose
-    waits claim 30 (more than the stores of one tick plus a load) must be reported."""
+    """The same analysis proves every `s_waitcnt vmcnt(11)` row wait (vmcnt(3) in the packed-trajectory
+    kernels): on every path at least that many vector memory instructions follow the row's load
+    (advisor r02).  A copy of the kernel whose waits claim more than the stores of one tick plus a
+    load (30, packed 4) must be reported."""
     src = os.path.join(ROOT, "footsies_gym_amd", "csrc", "fs_kernels.hip")
     text = open(src).read()
-    assert text.count("env_step<FM, P2, 11, kTabLds, GEOM>") >= 3
+    assert text.count("constexpr int kRowWait = PK ? 3 : 11;") == 1
     bad = tmp_path / "fs_kernels.hip"
-    bad.write_text(text.replace("env_step<FM, P2, 11, kTabLds, GEOM>", "env_step<FM, P2, 30, kTabLds, GEOM>"))
+    # (per-field waits claim 30, packed ones 4: one more than the 2 stores and a load)
+    bad.write_text(text.replace("constexpr int kRowWait = PK ? 3 : 11;", "constexpr int kRowWait = PK ? 4 : 30;"))
     # the one-lane kernel (fs_arena1.h, included from the same directory) waits with
     # vmcnt(12 (D - 1)), D = 3 slots: 24 is exact, so 25 must be reported
     one = open(os.path.join(ROOT, "footsies_gym_amd", "csrc", "fs_arena1.h")).read()
@@ -34,5 +38,5 @@ def test_wait_counts_are_proven_and_a_too_deep_wait_is_caught(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_async_loads.py"), str(bad)],
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 1, r.stdout[-2000:] + r.stderr[-2000:]
-    assert "vmcnt(30) copies" in r.stdout, r.stdout[-2000:]
+    assert "vmcnt(30) copies" in r.stdout and "vmcnt(4) copies" in r.stdout, r.stdout[-2000:]
     assert "vmcnt(25) copies" in r.stdout, r.stdout[-2000:]

@@ -371,3 +371,29 @@ def test_native_conversion_source_cache_follows_the_arrays():
     assert (info["frame"] == 7).all() and info["frame"].dtype == np.int64
     a["frame"][:] = 9
     assert (V.obs_info_from_outputs(a)[1]["frame"] == 9).all()
+
+
+def test_unpack_trajectory_layout():
+    """simulator.unpack_trajectory reads include/footsies.h's fs_packed_traj layout: per lane 16 B
+    (guard, move, action, hitstun bytes; move_frame, position floats; P1: frame, P2: terminated /
+    truncated bytes), the f64 reward beside it."""
+    from footsies_gym_amd.simulator import unpack_trajectory
+    T, N = 3, 5
+    lanes = np.zeros((T, N, 2, 16), np.uint8)
+    rng = np.random.default_rng(8)
+    guard, move, act, hs = (rng.integers(0, 200, (T, N, 2)).astype(np.uint8) for _ in range(4))
+    mf, pos = (rng.standard_normal((T, N, 2)).astype(np.float32) for _ in range(2))
+    frame = rng.integers(-1, 5000, (T, N)).astype(np.int32)
+    term = rng.integers(0, 2, (T, N)).astype(np.uint8)
+    lanes[..., 0], lanes[..., 1], lanes[..., 2], lanes[..., 3] = guard, move, act, hs
+    lanes[..., 4:8] = mf[..., None].view(np.uint8)
+    lanes[..., 8:12] = pos[..., None].view(np.uint8)
+    lanes[:, :, 0, 12:16] = frame[..., None].view(np.uint8)
+    lanes[:, :, 1, 12] = term
+    reward = rng.standard_normal((T, N))
+    v = unpack_trajectory({"lanes": lanes, "reward": reward, "final_lanes": lanes.copy()})
+    for k, want in (("guard", guard), ("move", move), ("action", act), ("hitstun", hs), ("move_frame", mf),
+                    ("position", pos), ("frame", frame), ("terminated", term), ("reward", reward)):
+        assert v[k].dtype == want.dtype and np.array_equal(v[k], want), k
+    assert not v["truncated"].any() and np.array_equal(v["final_frame"], frame)
+    assert "final_terminated" not in v and np.array_equal(v["final_position"], pos)
