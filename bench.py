@@ -40,6 +40,9 @@ LEG_TICKS = 1000        # ticks per region (and per launch) of the fused side le
 VENV_STEPS = 200        # timed FootsiesVectorEnv steps, after a warm-up into steady state
 
 
+LAYOUT_DEFAULT = "fields"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -53,6 +56,9 @@ def parse():
                          "(SURVEY 8(d) C4: 262144); overrides --envs")
     ap.add_argument("--mode", choices=["fused", "step"], default="fused")
     ap.add_argument("--chunk", type=int, default=1000, help="ticks per fs_step_n launch (fused mode; SURVEY 8(d) C3: n=1000)")
+    ap.add_argument("--layout", choices=["packed", "fields"], default=LAYOUT_DEFAULT,
+                    help="fused mode's trajectory: packed records (fs_step_n_packed, two stores per tick) or one "
+                         "array per field (fs_step_n); the other layout is timed beside as a secondary leg")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -486,12 +492,19 @@ def main():
     p1, p2 = sim.hash_actions(W + R * K, seed=args.seed, t0=0)
     torch.cuda.synchronize(dev)
     chunk = max(1, min(args.chunk, K))
-    traj = sim.alloc_trajectory(chunk)  # zero-filled: the pages are resident before timing
-    fs_step, fs_step_n = L.fs_step, L.fs_step_n
+    packed = args.layout == "packed"
+    alloc = sim.alloc_packed_trajectory if packed else sim.alloc_trajectory
+    traj = alloc(chunk)  # zero-filled: the pages are resident before timing
+    fs_step, fs_step_n, fs_step_n_packed = L.fs_step, L.fs_step_n, L.fs_step_n_packed
+    layout_flag = _abi.FS_KERNEL_PACKED if packed else 0
 
-    def make_runs(a1, a2, tr, ticks_per_launch):
+    def make_runs(a1, a2, tr, ticks_per_launch, packed=packed):
         b1, b2 = a1.data_ptr(), a2.data_ptr()
-        td = _abi.fs_outputs(**{k: tr[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+        if packed:
+            td = _abi.fs_packed_traj(lanes=tr["lanes"].data_ptr(), reward=tr["reward"].data_ptr(),
+                                     final_lanes=tr["final_lanes"].data_ptr())
+        else:
+            td = _abi.fs_outputs(**{k: tr[k].data_ptr() for k in _abi.OUTPUT_SPEC})
 
         def run_step(k0, n):
             for k in range(k0, k0 + n):
@@ -503,7 +516,10 @@ def main():
             k = k0
             while k < k0 + n:
                 m = min(ticks_per_launch, k0 + n - k)
-                rc = fs_step_n(h, m, C.c_void_p(b1 + k * N), C.c_void_p(b2 + k * N), 0, C.byref(td))
+                if packed:
+                    rc = fs_step_n_packed(h, m, C.c_void_p(b1 + k * N), C.c_void_p(b2 + k * N), C.byref(td))
+                else:
+                    rc = fs_step_n(h, m, C.c_void_p(b1 + k * N), C.c_void_p(b2 + k * N), 0, C.byref(td))
                 if rc:
                     check(rc, h)
                 k += m
@@ -589,6 +605,22 @@ def main():
         res[mode] = {"wall_s": wall, "region_walls_ms": [round(1e3 * w, 4) for w in walls],
                      "env_steps_per_s": world * N * K / wall, "ms_per_step": 1e3 * wall / K,
                      "rank_walls_ms": rank_values(mine)}
+    # fused mode: the other trajectory layout over the same action rows, timed the same way and
+    # reported beside (it continues the same handle's arenas)
+    other_layout = None
+    if args.mode == "fused":
+        otraj = (sim.alloc_trajectory if packed else sim.alloc_packed_trajectory)(chunk)
+        _, ofused = make_runs(p1, p2, otraj, chunk, packed=not packed)
+        ofused(W, min(K, 3))
+        torch.cuda.synchronize(dev)
+        local_walls = []
+        owalls = [timed(ofused, W + r * K, K) for r in range(R)]
+        ow = sorted(owalls)[len(owalls) // 2]
+        other_layout = {"trajectory": "one array per field (fs_step_n)" if packed else "packed records (fs_step_n_packed)",
+                        "value": world * N * K / ow, "ms_per_step": 1e3 * ow / K,
+                        "region_walls_ms": [round(1e3 * w, 4) for w in owalls],
+                        "kernel": L.fs_step_kernel(h, chunk, 0 if packed else _abi.FS_KERNEL_PACKED).decode()}
+        del otraj, ofused
     def leg_median(fn, k0, n):
         """A secondary leg: one untimed call (its kernels' first launch, staging buffers and the
         process group's first collective stay out of the timing), then R timed regions of n
@@ -649,20 +681,20 @@ def main():
             rfn, rlo, rhi = run_fused, W, W + R * K
         else:
             q1, q2 = sim.hash_actions(rt, seed=args.seed ^ 0x5A5A, t0=0)
-            rtraj = traj if rt == chunk else sim.alloc_trajectory(rt)
+            rtraj = traj if rt == chunk else alloc(rt)
             _, rfn = make_runs(q1, q2, rtraj, rt)
             rlo, rhi = 0, rt
             torch.cuda.synchronize(dev)
         kt, kmed, bytes_per_launch = roofline_at(rt, rfn, rlo, rhi, max(5, args.kernel_samples // 10))
         ticks = rt
         st_kt, st_kmed, st_bytes = roofline_at(chunk, run_fused, W, W + R * K, max(5, args.kernel_samples // 5))
-        kname = L.fs_step_kernel(h, rt, 0).decode()  # the kernel this launch shape runs (k_step_n1 from 2 x 64 x SIMDs arenas)
+        kname = L.fs_step_kernel(h, rt, layout_flag).decode()  # the kernel this launch shape runs (k_step_n1 from 2 x 64 x SIMDs arenas)
     else:
         kt, kmed, bytes_per_launch = roofline_at(1, run_step, W, W + R * K, args.kernel_samples)
         st_kt, st_kmed, st_bytes = kt, kmed, bytes_per_launch
         ticks = 1
         kname = L.fs_step_kernel(h, 1, 0).decode()
-    st_kname = L.fs_step_kernel(h, chunk if args.mode == "fused" else 1, 0).decode()
+    st_kname = L.fs_step_kernel(h, chunk if args.mode == "fused" else 1, layout_flag if args.mode == "fused" else 0).decode()
     achieved = bytes_per_launch / kt / 1e9
     tr = pmc_traffic(kname, N, ticks)
     issue = issue_profile(kname, N, ticks)
@@ -687,7 +719,9 @@ def main():
         "config": {"workload": ("C4 strong: %d arenas over %d GPUs" % (N * world, world) if args.global_envs else
                                 "C3: %d arenas/GPU" % N) + ", self-play random actions, P2 external, auto-reset same-step",
                    "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
-                   "ticks_per_launch": chunk if args.mode == "fused" else 1, "parallelism": "arena-shard x%d" % world},
+                   "ticks_per_launch": chunk if args.mode == "fused" else 1,
+                   "trajectory": ("packed records (fs_step_n_packed)" if packed else "one array per field (fs_step_n)")
+                   if args.mode == "fused" else None, "parallelism": "arena-shard x%d" % world},
         "ranks": {"world_size": dist.get_world_size() if grouped else 1,
                   "backend": dist.get_backend() if grouped else None,
                   "rank_walls_ms": res[args.mode]["rank_walls_ms"],
@@ -714,6 +748,7 @@ def main():
                                   "traffic": (pmc_traffic(st_kname, N, chunk if args.mode == "fused" else 1) or
                                               (None,))[0]},
         other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
+        "fused_other_layout": other_layout,
         "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
                                    "note": "fs_step with FS_ACT_HOST (PCIe-inclusive action hand-over); this and "
                                            "the gather legs: one untimed call, then the median of `regions` regions"},
