@@ -40,7 +40,7 @@ LEG_TICKS = 1000        # ticks per region (and per launch) of the fused side le
 VENV_STEPS = 200        # timed FootsiesVectorEnv steps, after a warm-up into steady state
 
 
-LAYOUT_DEFAULT = "fields"
+LAYOUT_DEFAULT = "packed"
 
 
 def parse():

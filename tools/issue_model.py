@@ -110,14 +110,17 @@ PROBE_KIND = {"fast": "v_add_u32", "vop3_op": "v_bfe_u32", "dpp_sdwa": "v_mov_b3
               "vopc": "v_cmp_gt_u32 vcc"}
 
 
-def occupancy_plateau(path):
-    """{arenas: env-steps/s} of the two-lane kernel (FOOTSIES_FUSED_LANES=2) in an occupancy sweep log."""
+def occupancy_plateau(path, packed=False):
+    """{arenas: env-steps/s} of the two-lane kernel in an occupancy sweep log: FOOTSIES_FUSED_LANES=2
+    lines of tools/ab_time.py (tools/occupancy_sweep.sh), or, for the packed-trajectory kernel, the
+    `packed` rates of tools/packed_ab.py at 65 536 / 131 072 / 262 144 arenas."""
     out = {}
     if not path or not os.path.exists(path):
         return out
-    n = None
+    pat = (r"packed\s+[\d.]+ us \(([\d.e+]+)\)" if packed else
+           r"FUSED_LANES=2\s+C3\s+[\d.]+ us \(([\d.e+]+) env-steps/s")
     for line in open(path):
-        m = re.search(r"FUSED_LANES=2\s+C3\s+[\d.]+ us \(([\d.e+]+) env-steps/s", line)
+        m = re.search(pat, line)
         if m:
             out.setdefault(len(out), float(m.group(1)))
     return out
@@ -158,7 +161,7 @@ def model(lib, kernel, probe_path, sq_path, sq_kernel, occ_path):
         "valu_pipe_frac_if_all_fast": round(wps * valu * cost["fast"] / (4.0 * quad), 3),
         "sources": {"probe": os.path.relpath(probe_path, ROOT), "sq": os.path.relpath(sq_path, ROOT)},
     }
-    occ = occupancy_plateau(occ_path)
+    occ = occupancy_plateau(occ_path, packed="packed" in kernel)
     if len(occ) >= 3:  # 2, 4, 8 waves per SIMD in the sweep's order (65 536, 131 072, 262 144 arenas)
         plateau = max(occ[1], occ[2])
         res.update({"rate_by_waves_per_simd": {"2": occ[0], "4": occ[1], "8": occ[2]},
