@@ -507,7 +507,9 @@ def test_bench_extras_legs():
     for leg in ("mixed_p2", "by_example"):
         assert d["actors_mode"][leg]["kernel"] == "fsk::k_step_n<0, 3>", d["actors_mode"]
         assert d["actors_mode"][leg]["value"] > 0
-    assert d["roofline"]["kernel"] == "fsk::k_step_n<0, 0>"
+    # the headline's fused trajectory is packed by default; the per-field layout is timed beside
+    assert d["roofline"]["kernel"] == "fsk::k_step_n_packed<0, 0>" and d["config"]["trajectory"].startswith("packed")
+    assert d["fused_other_layout"]["kernel"] == "fsk::k_step_n<0, 0>" and d["fused_other_layout"]["value"] > 0
     v = d["vector_env"]["numpy"]
     assert v["steps"] >= 200 and v["warmup_steps"] >= 200 and v["terminals_per_step"] > 0
 
