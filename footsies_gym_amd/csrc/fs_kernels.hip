@@ -1304,9 +1304,11 @@ __device__ __forceinline__ PkRec packed_record(const Lane& L, uint32_t w3) {
   int a = L.f.act;
   if (a == A_DEAD || a == A_WIN) a = A_STAND;  // FE:537-549
   const int mf = (a == A_STAND || a == A_FORWARD || a == A_BACKWARD) ? 0 : L.f.frame;  // FE:339-358
-  const uint32_t act = L.rec_count > 0 ? (uint32_t)L.rec & 0xffu : 0u;
+  const uint32_t act = L.rec_count > 0 ? (uint32_t)L.rec : 0u;  // a 3-bit input
   PkRec v;
-  v.x = ((uint32_t)L.f.guard & 0xffu) | (((uint32_t)a & 0xffu) << 8) | (act << 16) | (((uint32_t)L.f.stun & 0xffu) << 24);
+  // (guard is 0..3, the move index 0..16, the input 0..7: each fits its byte as it is; the shift
+  // keeps hitstun's low byte, the byte the per-field store keeps)
+  v.x = (uint32_t)L.f.guard | ((uint32_t)a << 8) | (act << 16) | ((uint32_t)L.f.stun << 24);
   v.y = __float_as_uint((float)mf);
   v.z = __float_as_uint(L.f.x);
   v.w = w3;
