@@ -132,7 +132,7 @@ def cpu_baseline(envs, seconds, seed):
                               "sample": "%d arenas x %d steps, 1 thread, %.1f s" % (envs, steps1, dt1)}}
 
 
-def fused_leg(torch, N, ticks, chunk, seed, device, rank, kind):
+def fused_leg(torch, N, ticks, chunk, seed, device, rank, kind, layout="fields"):
     """A fused-mode leg on its own handle, set up untimed; returns (run(k0, n), kernel name, close).
     kind "bot" = config C2's opponent at this size: P1 random (HBM), P2 the in-kernel BattleAI.
     kind "mixed_p2" = the per-arena actors (kActors, BC:158-167 P2_BOT): a remote-P2 handle with P2
@@ -153,8 +153,15 @@ def fused_leg(torch, N, ticks, chunk, seed, device, rank, kind):
         raise ValueError(kind)
     ext = kind == "mixed_p2"
     p1, p2 = sim.hash_actions(ticks, seed=seed, p2=ext)
-    traj = sim.alloc_trajectory(chunk)
-    td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+    # the headline's trajectory layout (packed records unless --layout fields)
+    packed = layout == "packed"
+    if packed:
+        traj = sim.alloc_packed_trajectory(chunk)
+        td = _abi.fs_packed_traj(lanes=traj["lanes"].data_ptr(), reward=traj["reward"].data_ptr(),
+                                 final_lanes=traj["final_lanes"].data_ptr())
+    else:
+        traj = sim.alloc_trajectory(chunk)
+        td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
     h, L = sim.handle, lib()
     b1 = p1.data_ptr()
     b2 = p2.data_ptr() if ext else None
@@ -164,11 +171,14 @@ def fused_leg(torch, N, ticks, chunk, seed, device, rank, kind):
         while k < k0 + n:
             m = min(chunk, k0 + n - k)
             q2 = C.c_void_p(b2 + k * N) if ext else None
-            rc = L.fs_step_n(h, m, C.c_void_p(b1 + k * N), q2, 0, C.byref(td))
+            if packed:
+                rc = L.fs_step_n_packed(h, m, C.c_void_p(b1 + k * N), q2, C.byref(td))
+            else:
+                rc = L.fs_step_n(h, m, C.c_void_p(b1 + k * N), q2, 0, C.byref(td))
             if rc:
                 check(rc, h)
             k += m
-    kname = L.fs_step_kernel(h, chunk, 0).decode()
+    kname = L.fs_step_kernel(h, chunk, _abi.FS_KERNEL_PACKED if packed else 0).decode()
 
     def close():
         sim.close()
@@ -770,7 +780,7 @@ def main():
                           ("actors_mode.by_example", "by_example")):
             try:
                 run_leg, leg_kernel, close_leg = fused_leg(torch, N, LEG_TICKS * (R + 1), LEG_TICKS, args.seed, local,
-                                                           rank, kind)
+                                                           rank, kind, layout=args.layout)
                 lw = leg_median(run_leg, LEG_TICKS, LEG_TICKS)
                 close_leg()
                 v = {"value": world * N * LEG_TICKS / lw, "ms_per_step": 1e3 * lw / LEG_TICKS,

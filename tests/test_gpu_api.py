@@ -503,9 +503,10 @@ def test_bench_extras_legs():
            "--chunk", "20", "--roofline-ticks", "20", "--no-cpu-baseline", "--kernel-samples", "5"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, check=True).stdout
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
-    assert d["p2_bot_mode"]["kernel"] == "fsk::k_step_n<0, 1>" and d["p2_bot_mode"]["value"] > 0
+    # (the side legs use the headline's trajectory layout, packed by default)
+    assert d["p2_bot_mode"]["kernel"] == "fsk::k_step_n_packed<0, 1>" and d["p2_bot_mode"]["value"] > 0
     for leg in ("mixed_p2", "by_example"):
-        assert d["actors_mode"][leg]["kernel"] == "fsk::k_step_n<0, 3>", d["actors_mode"]
+        assert d["actors_mode"][leg]["kernel"] == "fsk::k_step_n_packed<0, 3>", d["actors_mode"]
         assert d["actors_mode"][leg]["value"] > 0
     # the headline's fused trajectory is packed by default; the per-field layout is timed beside
     assert d["roofline"]["kernel"] == "fsk::k_step_n_packed<0, 0>" and d["config"]["trajectory"].startswith("packed")

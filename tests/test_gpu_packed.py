@@ -107,3 +107,12 @@ def test_packed_trajectory_argument_errors():
     from footsies_gym_amd._lib import lib  # the kernel a packed call runs, as rocprofv3 names it
     assert lib().fs_step_kernel(sim.handle, 4, _abi.FS_KERNEL_PACKED).decode() == "fsk::k_step_n_packed<0, 0>"
     torch.cuda.synchronize()
+
+
+def test_packed_trajectory_by_example():
+    """by_example (the bot plays P1 as well as P2: the kActors kernel with P1's rows unread)."""
+    from footsies_gym_amd.simulator import FootsiesSim
+    a = FootsiesSim(1500, p2_mode="bot", p1_mode="bot", seed=12)
+    b = FootsiesSim(1500, p2_mode="bot", p1_mode="bot", seed=12)
+    p1, _ = a.hash_actions(150, seed=0x31, p2=False)
+    _compare(a, b, 150, p1, None)
