@@ -207,11 +207,31 @@ class FootsiesSim:
                 check(lib().fs_step_masked(self._h, a1.ctypes.data, q2, m.ctypes.data, _abi.FS_ACT_HOST), self._h)
         return self._ready_out()
 
+    def _check_device(self, t, name, dtype, numel):
+        """A buffer the kernels read or write through its raw pointer: a contiguous torch tensor of
+        `dtype` on this handle's GPU with at least `numel` elements (anything else would hand the
+        kernel a host or foreign-device address, or let it run past the end)."""
+        torch = _torch()
+        if not (isinstance(t, torch.Tensor) and t.is_cuda and t.get_device() == self._dev_index and t.dtype == dtype
+                and t.is_contiguous() and t.numel() >= numel):
+            raise ValueError("%s: a contiguous %s tensor on %s with >= %d elements is required" % (
+                name, dtype, self.device, numel))
+
     def step_n(self, n, p1=None, p2=None, action_seed=0, trajectory=None):
         """n ticks in one kernel launch.  p1/p2: device uint8 [n][N] or None (on-device hashed
         actions).  trajectory: dict of device tensors shaped [n][N](,2) like ``alloc_trajectory``."""
+        torch = _torch()
+        n = int(n)
+        for name, a in (("p1", p1), ("p2", p2)):
+            if a is not None:
+                self._check_device(a, name, torch.uint8, n * self.num_envs)
         t = None
         if trajectory is not None:
+            for k in _abi.OUTPUT_SPEC:
+                if k in trajectory:
+                    dt, cols = _abi.OUTPUT_SPEC[k]
+                    self._check_device(trajectory[k], "trajectory[%r]" % k, getattr(torch, _TORCH_DTYPES[dt]),
+                                       n * self.num_envs * cols)
             t = _abi.fs_outputs(**{k: trajectory[k].data_ptr() for k in _abi.OUTPUT_SPEC if k in trajectory})
         check(lib().fs_step_n(self._h, int(n), None if p1 is None else C.c_void_p(p1.data_ptr()),
                               None if p2 is None else C.c_void_p(p2.data_ptr()), int(action_seed) & (2**64 - 1),
@@ -241,11 +261,18 @@ class FootsiesSim:
     def step_n_packed(self, n, p1, p2=None, trajectory=None):
         """step_n with device action rows p1 / p2 (uint8 [n][N]) into a packed trajectory
         (fs_step_n_packed: two stores per tick instead of ten; alloc_packed_trajectory)."""
+        torch = _torch()
+        n = int(n)
         traj = trajectory if trajectory is not None else self.alloc_packed_trajectory(n)
-        for name, t in traj.items():
-            if t is not None and (not t.is_contiguous() or t.device != self.device or t.shape[0] < n):
-                raise ValueError("packed trajectory buffer %r: contiguous, on %s, >= %d rows" % (name, self.device, n))
+        rows = n * self.num_envs
+        self._check_device(p1, "p1", torch.uint8, rows)
+        if p2 is not None:
+            self._check_device(p2, "p2", torch.uint8, rows)
+        self._check_device(traj["lanes"], "lanes", torch.uint8, rows * 2 * _abi.FS_PACKED_LANE_BYTES)
+        self._check_device(traj["reward"], "reward", torch.float64, rows)
         fl = traj.get("final_lanes")
+        if fl is not None:
+            self._check_device(fl, "final_lanes", torch.uint8, rows * 2 * _abi.FS_PACKED_LANE_BYTES)
         t = _abi.fs_packed_traj(lanes=traj["lanes"].data_ptr(), reward=traj["reward"].data_ptr(),
                                 final_lanes=None if fl is None else fl.data_ptr())
         check(lib().fs_step_n_packed(self._h, int(n), C.c_void_p(p1.data_ptr()),

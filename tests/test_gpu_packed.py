@@ -101,6 +101,15 @@ def test_packed_trajectory_argument_errors():
         sim.step_n_packed(4, p1, q2, trajectory=dict(traj, final_lanes=None))
     with pytest.raises(ValueError):  # a non-contiguous buffer
         sim.step_n_packed(4, p1, q2, trajectory=dict(traj, lanes=traj["lanes"].transpose(0, 1)))
+    # buffers the kernels would address raw are checked first: host, short or mistyped ones
+    with pytest.raises(ValueError):
+        sim.step_n_packed(4, p1.cpu(), q2, trajectory=traj)
+    with pytest.raises(ValueError):
+        sim.step_n_packed(4, p1[:2], q2, trajectory=traj)
+    with pytest.raises(ValueError):
+        sim.step_n(4, p1, q2.to(torch.int32))
+    with pytest.raises(ValueError):
+        sim.step_n(4, p1, q2, trajectory=dict(sim.alloc_trajectory(2)))
     delayed = FootsiesSim(64, p2_mode="external", frame_delay=2)
     with pytest.raises(FootsiesError):  # the delayed queue reads the per-field outputs
         delayed.step_n_packed(4, p1, q2)
