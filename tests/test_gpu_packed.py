@@ -118,6 +118,18 @@ def test_packed_trajectory_argument_errors():
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("dense", [True, False])
+def test_packed_trajectory_double_float_mode_and_sparse_reward(dense):
+    """The binary64-temporaries float model (FS_FLOAT_DOUBLE: the <1, P2> kernel instances) and
+    the sparse reward."""
+    from footsies_gym_amd.simulator import FootsiesSim
+    a = FootsiesSim(2000, p2_mode="external", seed=21, float_mode="double", dense_reward=dense)
+    b = FootsiesSim(2000, p2_mode="external", seed=21, float_mode="double", dense_reward=dense)
+    p1, q2 = a.hash_actions(200, seed=0x42)
+    exp = _compare(a, b, 200, p1, q2)
+    assert exp["terminated"].any()
+
+
 def test_packed_trajectory_by_example():
     """by_example (the bot plays P1 as well as P2: the kActors kernel with P1's rows unread)."""
     from footsies_gym_amd.simulator import FootsiesSim
