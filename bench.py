@@ -34,7 +34,13 @@ METRIC = "env-steps/sec (whole node) at 65 536 envs; bit-exact vs Unity ref"
 MI355X_SIMDS = 256 * 4  # CUs x SIMDs per CU (MI355X_MICROARCH.md)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (8.0 TB/s spec)
 STATE_BYTES = 96        # per arena per launch: 48 B state read + 48 B written (fs_kernels.hip layout)
-STEP_IO_BYTES = 40      # per env-step: 2 B actions in + 38 B outputs out (include/footsies.h fs_outputs)
+# per env-step, algorithmic (the useful bytes, whatever the layout): 2 B of actions in + 38 B of
+# outputs out (include/footsies.h fs_outputs' fields).  The headline's packed layout
+# (fs_step_n_packed, fs_packed_traj) writes those 38 B as two 16-B lane records + the 8-B reward,
+# i.e. 40 B out: 38 useful + 2 pad bytes in P2's record -- 42 B moved per env-step, 5 % above this
+# figure; `roofline.traffic_ratio` (PMC traffic / algorithmic bytes) reports the difference.
+STEP_IO_BYTES = 40
+PACKED_STEP_MOVED_BYTES = 42  # 2 B in + 40 B out per env-step in the packed layout (incl. the pad)
 XGMI_LINK_GBPS = 153.0  # per xGMI link and direction (task brief: 7 links x ~153 GB/s per MI355X)
 LEG_TICKS = 1000        # ticks per region (and per launch) of the fused side legs, whatever --steps is
 VENV_STEPS = 200        # timed FootsiesVectorEnv steps, after a warm-up into steady state
@@ -291,7 +297,7 @@ def vector_env_rate(torch, N, steps, device, warm=400):
             acts = list(torch.as_tensor(a1, device=torch.device("cuda", device)).unbind(0))
             r2 = list(torch.as_tensor(a2, device=torch.device("cuda", device)).unbind(0))
         opp = (lambda obs, info: r2[k[0]])
-        env = FootsiesVectorEnv(N, device=device, opponent=opp, output=kind, seed=0)
+        env = FootsiesVectorEnv(N, device=device, opponent=opp, output=kind, seed=0, retain_host_heap=kind == "numpy")
         env.reset(seed=0)
         for j in range(warm):
             k[0] = j
@@ -309,7 +315,8 @@ def vector_env_rate(torch, N, steps, device, warm=400):
         out[kind] = {"value": N * steps / dt, "ms_per_step": 1e3 * dt / steps, "steps": steps,
                      "warmup_steps": warm, "terminals_per_step": nterm / steps}
     out["config"] = ("FootsiesVectorEnv(%d, opponent=callable).step: numpy actions -> numpy obs/info dicts "
-                     "(D2H + conversion every step, final_observation dicts for the terminated arenas), and "
+                     "(D2H + conversion every step, final_observation dicts for the terminated arenas; retain_host_heap=True, "
+                     "the opt-in glibc tuning), and "
                      "output='torch' (device tensors in/out); steady state after the warm-up" % N)
     return out
 
@@ -742,10 +749,13 @@ def main():
                            "(host wall clock, max over ranks); value = the median region"},
         "roofline": {"bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": tr[0] if tr else None,
+                     "traffic_ratio": (tr[0] / bytes_per_launch) if tr else None,
                      "traffic_source": tr[1] if tr else None,
+                     "layout_bytes_per_launch": (N * (STATE_BYTES + ticks * PACKED_STEP_MOVED_BYTES)
+                                                 if args.mode == "fused" and packed else bytes_per_launch),
                      "kernel": kname, "ticks_per_launch": ticks, "avg_launch_us": kt * 1e6,
                      "median_launch_us": kmed * 1e6, "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "note": "avg_launch_us: back-to-back launch period (one HIP event pair over the launches), median_launch_us: per-launch event pairs (their records add a few us between kernels); achieved / peak / frac: the HBM roofline of the kernel's algorithmic bytes; `bound` "
+                     "note": "avg_launch_us: back-to-back launch period (one HIP event pair over the launches), median_launch_us: per-launch event pairs (their records add a few us between kernels); achieved / peak / frac: the HBM roofline of the kernel's algorithmic bytes (per arena 96 B of state per launch, per env-step 2 B of actions in + 38 B of outputs out); the packed layout moves 2 B in + 40 B out per env-step (38 useful + 2 pad bytes in P2's 16-B record), layout_bytes_per_launch; traffic_ratio = PMC traffic / algorithmic bytes; `bound` "
                              "names what binds it: the SIMDs' instruction issue (issue.issue_frac, the rate over the "
                              "same kernel's plateau at 4-8 waves per SIMD) when a SIMD-level issue model of this "
                              "kernel is committed",

@@ -6,7 +6,7 @@ the test-side oracle binding (``oracle/binding.py``) agree on layouts.
 """
 import ctypes as C
 
-FS_ABI_VERSION = 4
+FS_ABI_VERSION = 5
 
 FS_OK = 0
 FS_E_INVALID = -1
@@ -190,7 +190,8 @@ LIB_FUNCTIONS = {
     "fs_num_envs": (C.c_int, [C.c_void_p]),
     "fs_steps_taken": (C.c_uint64, [C.c_void_p]),
     "fs_step_kernel": (C.c_char_p, [C.c_void_p, C.c_int, C.c_int]),
-    "fs_host_convert": (C.c_int, [C.POINTER(fs_outputs), C.c_void_p, C.c_int64, C.POINTER(fs_host_arrays), C.c_int]),
+    "fs_host_convert": (C.c_int, [C.POINTER(fs_outputs), C.c_int64, C.c_void_p, C.c_int64, C.POINTER(fs_host_arrays),
+                                  C.c_int]),
     "fs_destroy": (None, [C.c_void_p]),
     "fs_last_error": (C.c_char_p, [C.c_void_p]),
 }

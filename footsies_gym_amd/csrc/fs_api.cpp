@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -780,10 +781,14 @@ FS_API int fs_set_state(fs_handle h, const fs_arena_state* host_in) {
   if (e != hipSuccess) return set_err(h, FS_E_DEVICE, "fs_set_state: %s", hipGetErrorString(e));
   for (int i = 0; i < h->n; i++) set_p2bot_mirror(h, (size_t)i, host_in[i].p2_bot);
   // every arena was replaced: the general-geometry tick is needed iff a loaded fighter is off the
-  // ground or faces the other way (-0.0 counts as 0: it moves no box and doubles to itself)
+  // ground or faces the other way.  y is tested by its bits: a -0.0 moves no box, but the pushes
+  // keep it (-0.0 + -0.0) and the round start writes +0.0 (SetupBattleStart, F:120-135), and only
+  // the general-geometry tick carries y through a step (the standard one never writes it back)
   bool geom = false;
   for (int i = 0; i < h->n && !geom; i++)
-    for (int k = 0; k < 2; k++) geom = geom || host_in[i].f[k].position_y != 0.0f || host_in[i].f[k].facing_flipped;
+    for (int k = 0; k < 2; k++)
+      geom = geom || std::signbit(host_in[i].f[k].position_y) || host_in[i].f[k].position_y != 0.0f ||
+             host_in[i].f[k].facing_flipped;
   h->geom = geom;
   return FS_OK;
 }
@@ -899,9 +904,15 @@ class HostPool {
 };
 }  // namespace
 
-FS_API int fs_host_convert(const fs_outputs* src, const int64_t* rows, int64_t n, const fs_host_arrays* dst,
-                           int threads) {
-  if (!src || !dst || n < 0) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: src, dst and n >= 0 required");
+FS_API int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n,
+                           const fs_host_arrays* dst, int threads) {
+  if (!src || !dst || n < 0 || n_src < 0)
+    return set_err(nullptr, FS_E_INVALID, "fs_host_convert: src, dst, n >= 0 and n_src >= 0 required");
+  if (!rows && n > n_src) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: n exceeds the source's n_src rows");
+  if (rows)  // every source row the conversion will read, checked before any thread starts
+    for (int64_t i = 0; i < n; ++i)
+      if (rows[i] < 0 || rows[i] >= n_src)
+        return set_err(nullptr, FS_E_INVALID, "fs_host_convert: rows[i] outside [0, n_src)");
   const fs_outputs S = *src;
   const fs_host_arrays D = *dst;
   if ((D.guard || D.info_guard) && !S.guard) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: no guard source");

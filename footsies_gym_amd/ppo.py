@@ -9,7 +9,9 @@ One iteration:
    the same device. The observation before tick t is the output of tick t - 1 (after a
    same-step auto-reset that is the fresh round's state, so a terminal tick's successor is
    never bootstrapped through: done masks it).
-3. `epochs` x `minibatches` clipped-surrogate updates of the actor and critic, fp32.  With
+3. `epochs` x `minibatches` clipped-surrogate updates of the actor and critic (fp32 Adam; the
+   gradients' 64x64 hidden layer on split-bf16 MFMAs by default since round 4,
+   `learner_precision="fp32"` for fp32 FMAs).  With
    `learner="hip"` (the default) each minibatch's loss and gradient come from one fused
    forward + backward kernel per network (fs_ppo_grad, csrc/fs_learn.hip) straight into the
    parameters' .grad; `learner="torch"` runs the same loss through torch autograd (the
@@ -19,7 +21,9 @@ One iteration:
    recomputed in fp32 (`old_logp="fp32"`, first ratio exactly 1).  Either way the iteration
    reports how far the two are apart: `kl_behaviour_fp32`, the sample estimate
    E_a~behaviour[log p_bf16(a) - log p_fp32(a)] of KL(bf16 actor || fp32 actor), and
-   `logp_abs_diff`, the mean |log p_bf16(a) - log p_fp32(a)|.
+   `logp_abs_diff`, the mean |log p_bf16(a) - log p_fp32(a)|.  The fp32 log-probs and the
+   critic values come from fs_ppo_eval at fp32 FMAs (FS_PPO_FP32) whatever the learner's
+   precision; only the gradients use `learner_precision`.
 4. The new actor weights are copied into the rollout's device buffers (no reallocation).
 
 Nothing leaves the GPU inside an iteration, and the simulator never waits on the host.
@@ -195,10 +199,14 @@ class PPOGrad:
         if moved:
             self._bind()
 
-    def evaluate(self, x, actions=None, n_logp=0):
+    def evaluate(self, x, actions=None, n_logp=0, precision=None):
         """fs_ppo_eval: (critic(x) [n], log_softmax(actor(x[:n_logp]))[actions] [n_logp] or None),
-        fp32, without gradient; x: device [n, 8] fp32, actions: device uint8 [n_logp]."""
+        without gradient; x: device [n, 8] fp32, actions: device uint8 [n_logp].  `precision`:
+        "fp32" or "split_bf16" for this call (default: the learner's own)."""
         torch = _torch()
+        if precision is not None and precision not in self.PRECISIONS:
+            raise ValueError("precision must be one of %s" % sorted(self.PRECISIONS))
+        prec = self._prec if precision is None else self.PRECISIONS[precision]
         if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES or not x.is_contiguous():
             raise ValueError("x must be a contiguous [n, 8] float32 tensor")
         n = x.shape[0]
@@ -214,7 +222,7 @@ class PPOGrad:
                                    n_logp, C.byref(self._mlps[0]), C.byref(self._mlps[1]),
                                    C.c_void_p(values.data_ptr()), C.c_void_p(logp.data_ptr() if n_logp else None),
                                    C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), C.c_void_p(stream),
-                                   self._prec))
+                                   prec))
         return values, logp
 
     def __call__(self, rows, clip, vf_coef, ent_coef):
@@ -382,7 +390,9 @@ class PPOTrainer:
             a = actions.reshape(M)
             behav = self.logp.reshape(M)  # what the kernel sampled with (bf16 actor)
             if self._grad is not None:  # both forward passes, GAE and the sample table: five launches
-                v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk)
+                # always at fp32 FMAs, whatever the learner's precision: old32 is the fp32 reference
+                # the KL diagnostic and old_logp="fp32" are defined against
+                v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk, precision="fp32")
                 values = v.view(T + 1, N)
                 adv, ret = gae_device(rewards, dones, values, self.gamma, self.lam)
                 old = behav if self.old_logp == "behaviour" else old32

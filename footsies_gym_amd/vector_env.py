@@ -43,8 +43,10 @@ def retain_host_heap():
     unmaps them on free, so every step re-faults every page of its arrays: measured in the build
     container, the host conversion of one step took 5.2 ms, 1.7 ms once glibc keeps blocks below
     256 MB on its heap (mallopt M_MMAP_THRESHOLD) and stops trimming the heap (M_TRIM_THRESHOLD).
-    Process-wide, done once, on the first numpy-output FootsiesVectorEnv; FOOTSIES_NO_MALLOPT=1
-    leaves the allocator alone.  Returns whether the settings were applied."""
+    Process-wide and irreversible (freed memory up to 1 GB then stays resident in this process),
+    so it is opt-in: call it, or create a numpy-output FootsiesVectorEnv with
+    ``retain_host_heap=True``; FOOTSIES_NO_MALLOPT=1 refuses it.  Returns whether the settings
+    were applied."""
     global _HEAP_RETAINED
     import os
     if _HEAP_RETAINED or os.environ.get("FOOTSIES_NO_MALLOPT") == "1":
@@ -59,6 +61,8 @@ def retain_host_heap():
         _HEAP_RETAINED = False
     return _HEAP_RETAINED
 
+
+_tune_heap = retain_host_heap  # (the constructor's flag of the same name shadows it there)
 
 _SRC_DTYPES = {"guard": np.uint8, "move": np.uint8, "move_frame": np.float32, "position": np.float32,
                "reward": np.float64, "terminated": np.uint8, "truncated": np.uint8, "frame": np.int32,
@@ -151,7 +155,8 @@ def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
     views = {name: np.ndarray((n, c) if c else (n,), dt, blocks[b], off)
              for (name, dt, c, _), (b, off) in zip(members, offs)}
     r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
-    check(lib().fs_host_convert(C.byref(so), None if r is None else r.ctypes.data, n, C.byref(dst),
+    n_src = len(out[prefix + "frame"])
+    check(lib().fs_host_convert(C.byref(so), n_src, None if r is None else r.ctypes.data, n, C.byref(dst),
                                 host_threads()))
     del keep  # (the converted sources lived over the call)
     obs = {k: views[k] for k in ("guard", "move", "move_frame", "position")}
@@ -202,6 +207,8 @@ def step_result_from_outputs(out, autoreset_mode="same_step"):
         idx = np.nonzero(term)[0]
         # only the terminated arenas' final outputs are converted
         fobs, finfo, _ = _host_convert(out, "final_", idx, len(idx), False, info_copies=False)
+        for a in fobs.values():  # shared by final_observation and final_info below: read-only rows
+            a.setflags(write=False)
         final_obs = np.empty(len(term), dtype=object)
         final_info = np.empty(len(term), dtype=object)
         # Per-arena dicts (gymnasium 0.29's contract: one dict per terminated env, None elsewhere),
@@ -238,6 +245,9 @@ class FootsiesVectorEnv(_VectorEnvBase):
     ``by_example`` (FE:83-84, 118, 230-232): the in-game bot plays P1 as well and the agent only
     observes -- ``step`` ignores its actions (FE:522-523).
     ``output="torch"`` returns device tensors (zero-copy) instead of numpy.
+    ``retain_host_heap=True`` (numpy output, opt-in): tune glibc for the step's large fresh arrays
+    (``retain_host_heap()``: mallopt M_MMAP_THRESHOLD 256 MB, M_TRIM_THRESHOLD 1 GB) -- process-wide,
+    so off by default; at 65 536 arenas it saves the re-faulting of ~9 MB of pages per step.
     (``_host_outputs``, internal, numpy output only: the kernels write the outputs into pinned host
     memory -- FootsiesSim ``host_outputs`` -- instead of HBM, so a step needs no device-to-host copy
     of its own.  The default for numpy output: at 65 536 arenas a step took 0.45-0.46 ms so, against
@@ -251,7 +261,7 @@ class FootsiesVectorEnv(_VectorEnvBase):
 
     def __init__(self, num_envs, device=0, opponent=None, dense_reward=True, frame_delay=0,
                  autoreset_mode="same_step", float_mode="strict", seed=0, vs_player=False, by_example=False,
-                 output="numpy", _host_outputs=None):
+                 output="numpy", retain_host_heap=False, _host_outputs=None):
         if vs_player:
             raise ValueError("vs_player needs a human at the game window; not available in the simulator")
         if not 0 <= int(frame_delay) <= _abi.FS_MAX_FRAME_DELAY:
@@ -264,8 +274,8 @@ class FootsiesVectorEnv(_VectorEnvBase):
             raise ValueError("host-memory outputs serve the numpy output only")
         self.num_envs = int(num_envs)
         self.output = output
-        if output == "numpy":
-            retain_host_heap()
+        if output == "numpy" and retain_host_heap:
+            _tune_heap()
         self.autoreset_mode = autoreset_mode
         self.dense_reward = dense_reward
         self._opponent = opponent

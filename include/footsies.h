@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 4
+#define FS_ABI_VERSION 5
 
 /* error codes */
 #define FS_OK 0
@@ -402,11 +402,14 @@ typedef struct fs_host_arrays {
 } fs_host_arrays;
 
 /* Convert host copies of step outputs (`src`: the fs_outputs layout in host memory, e.g. the
- * pinned copy of fs_outputs_get's buffers; only its first ten members are read) into `dst`,
- * over `threads` host threads (a pool kept by the library).  Row i of dst is row rows[i] of src
- * (rows NULL: row i), for i < n -- so the terminal records of the arenas that ended a step are
- * converted by passing the final_* arrays as src's first members and the terminated rows. */
-int fs_host_convert(const fs_outputs* src, const int64_t* rows, int64_t n, const fs_host_arrays* dst, int threads);
+ * pinned copy of fs_outputs_get's buffers, `n_src` rows each; only its first ten members are
+ * read) into `dst`, over `threads` host threads (a pool kept by the library).  Row i of dst is
+ * row rows[i] of src (rows NULL: row i), for i < n -- so the terminal records of the arenas that
+ * ended a step are converted by passing the final_* arrays as src's first members and the
+ * terminated rows.  FS_E_INVALID (nothing written) when a row index is outside [0, n_src) or,
+ * without rows, n > n_src.  (ABI 5 added n_src.) */
+int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n, const fs_host_arrays* dst,
+                    int threads);
 
 /* Pack the current outputs into one FS_RECORD_BYTES record per arena at dst (device,
  * [N][40] bytes): guard[2] move[2] action[2] hitstun[2] u8, terminated u8, truncated

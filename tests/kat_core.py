@@ -31,7 +31,7 @@ Assets/Fighter/F00/F00_AttackDataContainer.asset.
 """
 import numpy as np
 
-from tests.kat_combat import ACTIONS, ATTACKS, DT, F32, approach, run, step_x, velocity
+from tests.kat_combat import ACTIONS, ATTACKS, DT, F32, approach, load, run, step_x, velocity
 
 L, R, A = 1, 2, 4
 STAND, FORWARD, BACKWARD, DASH_F, DASH_B = 0, 1, 2, 10, 11
@@ -364,7 +364,155 @@ def kat_guard_break_reserve(backend):
     assert (st[52]["p1Move"], st[52]["p1MoveFrame"]) == (GUARD_BREAK, 1) and st[52]["p2MoveFrame"] == 5
 
 
+# ---------------------------------------------------------------------------------------------
+# the attack table's row for every attack: blocked, landed, guard broken
+# ---------------------------------------------------------------------------------------------
+B_ATTACK, DAMAGE, GUARD_M, GUARD_STAND = 105, 200, 301, 305
+HALF_HURT = F32(0.75)  # F00.asset baseHurtBoxRect width 1.5, a centred BoxBase (F:8-26)
+PUSH_W = F32(1.4)      # F00.asset basePushBoxRect width, a Rect whose x is the left edge (BC:483-501)
+# attacker action -> (attack ID of its real hitbox, the frame loaded: the one before the box is out)
+ATTACK_OF = {N_ATTACK: (1, 3), B_ATTACK: (2, 2), N_SPECIAL: (10, 10), B_SPECIAL: (11, 1)}
+
+
+def _real_hitbox(action, frame):
+    boxes = [h for h in ACTIONS[action]["hitboxes"] if not h["proximity"] and h["win"][0] <= frame <= h["win"][1]]
+    assert len(boxes) == 1, (action, frame)
+    return boxes[0]
+
+
+def _table_hit(backend, attacker, action, guard, block, gap):
+    """One arena loaded (STATE_LOAD) with the attacker in `action` one frame before its real
+    hitbox comes out and the defender standing `gap` apart, holding back when `block` (its back
+    is away from the attacker: P1 Left, P2 Right; F:642-666) with its guard loaded at `guard`.
+    Tick 0: the attacker's frame advances into the hitbox window and it moves by that frame's
+    velocity (N_SPECIAL 5, B_SPECIAL 3, the attacks none); a blocking defender walks back
+    (STAND -> BACKWARD, always cancelable, F:265-283) by 1.8 * dt; the pushboxes stay apart and
+    the real hitbox reaches the base hurtbox (checked here in float32), so NotifyDamaged runs on
+    tick 0.  Returns per-tick env states, outputs and canonical states, and both x after tick 0."""
+    atk_id, f0 = ATTACK_OF[action]
+    hb = _real_hitbox(action, f0 + 1)
+    assert hb["attack_id"] == atk_id
+    a_sign = 1 if attacker == 0 else -1         # P1 faces right, P2 left
+    xa = F32(-a_sign * gap / 2)
+    xd = F32(a_sign * gap / 2)
+    fresh(backend)
+    atk_rec, def_rec = (action, f0), (STAND, 0)
+    p1, p2 = ((xa,) + atk_rec, (xd,) + def_rec) if attacker == 0 else ((xd,) + def_rec, (xa,) + atk_rec)
+    load(backend, p1, p2)
+    if guard != 3:
+        s = backend.state()
+        s["f"][0, 1 - attacker]["guard"] = guard
+        backend.set_state(s)
+    xa1 = step_x(xa, velocity(action, f0 + 1), a_sign)
+    xd1 = step_x(xd, 1.8, -a_sign, walk="backward") if block else xd
+    c = F32(xa1 + F32(F32(hb["rect"][0]) * F32(a_sign)))
+    lo, hi = F32(c - F32(F32(hb["rect"][2]) / F32(2))), F32(c + F32(F32(hb["rect"][2]) / F32(2)))
+    assert lo <= F32(xd1 + HALF_HURT) and F32(xd1 - HALF_HURT) <= hi, (action, lo, hi, xd1)
+    left, right = (xa1, xd1) if attacker == 0 else (xd1, xa1)
+    assert F32(left + PUSH_W) < right  # no character push (strict Rect overlap, BC:485-499)
+    back = R if attacker == 0 else L  # the defender's back: P2's is Right, P1's Left
+    d_in = back if block else 0
+    ins = (lambda t: 0, lambda t: d_in) if attacker == 0 else (lambda t: d_in, lambda t: 0)
+    st, out, cs = {}, {}, {}
+    for t in range(40):
+        o = backend.step(_a(ins[0](t)), _a(ins[1](t)))
+        st[t] = backend.env_state()[0].copy()
+        out[t] = {k: np.array(v, copy=True) for k, v in o.items()}
+        cs[t] = backend.state()[0].copy()
+        if o["terminated"][0]:
+            break
+    return st, out, cs, xa1, xd1
+
+
+def kat_attack_table_rows(backend):
+    """F:446-454 picks the stun from the attacker's AttackData row by DamageResult, and NotifyDamaged
+    (F:357-398) the defender's action from the same row (ATK:14-54):
+
+      attack      damageAction  guardAction  hitStun  guardStun  guardBreakStun  vital dmg
+      N_ATTACK 1      200          306          12       12           30            0
+      B_ATTACK 2      200          305          12       12           30            0
+      N_SPECIAL 10    500          301           0       15           30            1
+      B_SPECIAL 11    500          301           0       15           30            1
+
+    For each attack, attacking as P1 and as P2 (the collision's two trade phases, BC:523-586):
+    * blocked (the defender walks back, BACKWARD counts as blocking, F:370-371): guard 3 -> 2,
+      guardAction at frame 0, guardStun on both fighters, dense reward -0.3 / +0.3 for the
+      defender's guard (FE:393-394), vital kept; the stun counts down with both frames frozen
+      (F:149-154) and, on the tick it reaches 0, the defender moves by its guard action's frame-0
+      velocity (ACT/GUARD_*.asset) away from the attacker;
+    * guard broken (guard loaded at 0, blocking): guard stays 0, guardAction with GUARD_BREAK
+      reserved, guardBreakStun 30 on both, reward 0; on the tick the stun reaches 0 the reserve
+      is taken (F:212-218): GUARD_BREAK frame 0;
+    * landed (standing): the attacks give DAMAGE with hitStun 12 and guard 3 -> 2 (guard damage
+      applies unblocked too); the specials kill: DEAD, terminated, the episode's return +-1 with
+      the guard drop included (FE:388-405), hitStun 0 on both;
+    * landed on a guard of 0 (isGuardBreak set, but not blocking): the damage branch, DAMAGE with
+      hitStun 12 -- never the guard-break stun -- and reward 0."""
+    guard_row = {N_ATTACK: GUARD_CROUCH, B_ATTACK: GUARD_STAND, N_SPECIAL: GUARD_M, B_SPECIAL: GUARD_M}
+    for action, (atk_id, _) in ATTACK_OF.items():
+        a = ATTACKS[atk_id]
+        assert a["guard_action"] == guard_row[action] and a["guard_damage"] == 1 and a["guard_break_stun"] == 30
+        assert (a["damage_action"], a["hit_stun"], a["guard_stun"], a["vital_damage"]) == (
+            (DAMAGE, 12, 12, 0) if action in (N_ATTACK, B_ATTACK) else (500, 0, 15, 1)), action
+        special = action in (N_SPECIAL, B_SPECIAL)
+        gap = 1.6 if action == B_SPECIAL else 2.0
+        for attacker in (0, 1):
+            A_, D_ = ("p1", "p2") if attacker == 0 else ("p2", "p1")
+            sgn = 1.0 if attacker == 0 else -1.0  # dense reward: + when P2's guard drops
+            dsign = -1 if attacker == 0 else 1    # the defender's facing sign
+            label = (action, attacker)
+            # blocked
+            st, out, cs, xa1, xd1 = _table_hit(backend, attacker, action, 3, True, gap)
+            h, stun = st[0], a["guard_stun"]
+            assert (h[D_ + "Move"], h[D_ + "MoveFrame"], h[D_ + "Guard"], h[D_ + "Vital"]) == (
+                a["guard_action"], 0, 2, 1), (label, h[D_ + "Move"], h[D_ + "Guard"])
+            assert (h[A_ + "Move"], h[A_ + "MoveFrame"]) == (action, ATTACK_OF[action][1] + 1), label
+            assert (h[A_ + "Hitstun"], h[D_ + "Hitstun"]) == (stun, stun), (label, h[A_ + "Hitstun"])
+            assert out[0]["reward"][0] == sgn * 0.3 and not out[0]["terminated"][0], label
+            assert h[D_ + "Position"] == xd1 and h[A_ + "Position"] == xa1, label
+            for t in range(1, stun):
+                s = st[t]
+                assert (s[D_ + "Move"], s[D_ + "MoveFrame"], s[D_ + "Hitstun"]) == (a["guard_action"], 0, stun - t), (label, t)
+                assert (s[A_ + "MoveFrame"], s[A_ + "Hitstun"]) == (ATTACK_OF[action][1] + 1, stun - t), (label, t)
+                assert s[D_ + "Position"] == xd1, (label, t)
+            s = st[stun]
+            assert s[D_ + "Hitstun"] == 0 and s[D_ + "Position"] == step_x(xd1, velocity(a["guard_action"], 0), dsign), label
+            # guard broken
+            st, out, cs, xa1, xd1 = _table_hit(backend, attacker, action, 0, True, gap)
+            h = st[0]
+            assert (h[D_ + "Move"], h[D_ + "MoveFrame"], h[D_ + "Guard"], h[D_ + "Vital"]) == (
+                a["guard_action"], 0, 0, 1), (label, h[D_ + "Move"])
+            assert (h[A_ + "Hitstun"], h[D_ + "Hitstun"]) == (30, 30) and out[0]["reward"][0] == 0.0, label
+            assert int(cs[0]["f"][1 - attacker]["reserve_action_id"]) == GUARD_BREAK, label
+            for t in range(1, 30):
+                assert (st[t][D_ + "Move"], st[t][D_ + "Hitstun"]) == (a["guard_action"], 30 - t), (label, t)
+            s = st[30]
+            assert (s[D_ + "Move"], s[D_ + "MoveFrame"], s[D_ + "Hitstun"]) == (GUARD_BREAK, 0, 0), (label, s[D_ + "Move"])
+            assert s[D_ + "Position"] == step_x(xd1, velocity(GUARD_BREAK, 0), dsign), label
+            # landed, then landed on a guard of 0
+            for guard in (3, 0):
+                st, out, cs, xa1, xd1 = _table_hit(backend, attacker, action, guard, False, gap)
+                o = out[0]
+                if special:  # vital 1 -> 0: DEAD, the battle is over this tick (BC:212-218)
+                    assert o["terminated"][0] == 1, (label, guard)
+                    r0 = sgn * 0.3 if guard else 0.0  # FE:393-404 in its float64 order
+                    assert o["reward"][0] == r0 + (sgn * 1.0 - r0), (label, guard, o["reward"][0])
+                    dk = 0 if attacker == 1 else 1
+                    assert o["final_move"][0, dk] == 0 and o["final_guard"][0, dk] == (2 if guard else 0), (label, guard)
+                    assert tuple(o["final_hitstun"][0]) == (0, 0), (label, guard)  # hitStun 0
+                    continue
+                h = st[0]
+                assert (h[D_ + "Move"], h[D_ + "MoveFrame"], h[D_ + "Vital"]) == (DAMAGE, 0, 1), (label, guard, h[D_ + "Move"])
+                assert h[D_ + "Guard"] == (2 if guard else 0) and (h[A_ + "Hitstun"], h[D_ + "Hitstun"]) == (12, 12), (label, guard)
+                assert out[0]["reward"][0] == (sgn * 0.3 if guard else 0.0) and not o["terminated"][0], (label, guard)
+                assert int(cs[0]["f"][1 - attacker]["reserve_action_id"]) == -1, (label, guard)
+                s = st[12]
+                assert (s[D_ + "Move"], s[D_ + "Hitstun"]) == (DAMAGE, 0), (label, guard)
+                assert s[D_ + "Position"] == step_x(xd1, velocity(DAMAGE, 0), dsign), (label, guard)
+
+
 ALL = {
+    "attack_table_rows": kat_attack_table_rows,
     "b_special_windows": kat_b_special_windows,
     "dash_edges": kat_dash_edges,
     "intro_stale_input": kat_intro_stale_input,
@@ -375,6 +523,8 @@ ALL = {
 
 # The C# paths each scenario pins (DESIGN.md section 3 reproduces this table)
 PINS = {
+    "attack_table_rows": "F:357-398, 446-454 + ATK:14-54: every attack's guardAction / guardStun, damageAction / hitStun, "
+                         "guardBreakStun with GUARD_BREAK reserved, as P1 and as P2 (BC:523-586)",
     "b_special_windows": "AD:150-161 first-match GetMovementData over ACT/B_SPECIAL.asset:14-83's overlapping windows",
     "dash_edges": "F:585-635 dash parsers at dashAllowFrame 9 (tap gap 8/9, hold 8/9, interrupt, P2 facing)",
     "intro_stale_input": "BC:183-200, 329-345 Intro tick input after SetupBattleStart's ClearInput (F:120-135)",

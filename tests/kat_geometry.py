@@ -223,7 +223,30 @@ def kat_round_start_restores_geometry(backend):
                                                         F32(_DATA["stage"]["p2_start_x"]))
 
 
+def kat_negative_zero_y(backend):
+    """position.y loaded as -0.0 (STATE_LOAD, F:741-744) is kept bit for bit while the fighter
+    stands and is pushed (each push adds y to itself: -0.0 + -0.0 = -0.0, BC:491-498, 511-515),
+    and the round start writes +0.0 (SetupBattleStart's new Vector2(-2f, 0f), BC:264-265, F:120-135).
+    P1 stands past the stage edge (x -5.5: pushed in, y doubled), then is loaded with vital 0 so
+    the next tick ends the round and the same-step auto-reset runs the round start."""
+    fresh(backend)
+    load_geom(backend, {"x": -5.5, "y": -0.0}, {"x": 2.0, "y": -0.0})
+    f = backend.state()[0]["f"]
+    assert np.signbit(f[0]["position_y"]) and np.signbit(f[1]["position_y"])
+    x1, y1, _, y2 = _expect_standing(backend, F32(-5.5), F32(-0.0), F32(2.0), F32(-0.0), 3)
+    f = backend.state()[0]["f"]
+    assert x1 > F32(-5.5) and np.signbit(f[0]["position_y"]) and np.signbit(f[1]["position_y"])
+    s = backend.state()
+    s["f"][0, 0]["vital"] = 0
+    backend.set_state(s)
+    assert backend.step(_a(0), _a(0))["terminated"][0] == 1
+    f = backend.state()[0]["f"]
+    assert not np.signbit(f[0]["position_y"]) and not np.signbit(f[1]["position_y"])
+    assert f[0]["position_y"] == 0 and f[1]["position_y"] == 0
+
+
 ALL = {
+    "negative_zero_y": kat_negative_zero_y,
     "flipped_walk": kat_flipped_walk,
     "airborne_not_pushed": kat_airborne_not_pushed,
     "stage_push_doubles_y": kat_stage_push_doubles_y,

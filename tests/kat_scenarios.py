@@ -199,7 +199,7 @@ def kat_guard_break(backend):
         if s2["p1Guard"] < s["p1Guard"] or (s["p1Guard"] == 0 and s2["p1Hitstun"] == 30 and broke_at is None
                                              and s2["p1Move"] in (GUARD_M, GUARD_STAND, GUARD_CROUCH)):
             events.append((t, int(s["p1Guard"]), int(s2["p1Guard"]), int(s2["p1Move"]), int(s2["p1Hitstun"]),
-                           float(out["reward"][0])))
+                           float(out["reward"][0]), int(s2["p2Move"])))
             if s["p1Guard"] == 0:
                 broke_at = t
         if broke_at is not None and s2["p1Move"] == GUARD_BREAK:
@@ -207,9 +207,13 @@ def kat_guard_break(backend):
             break
         last = s2
     assert [(e[1], e[2]) for e in events[:3]] == [(3, 2), (2, 1), (1, 0)], events
+    # the row of the attack that landed (P2's action, frozen in its hit-stop): guardAction and
+    # guardStun, or guardBreakStun on the fourth hit (F:370-384, 446-454; ATK:14-54)
+    row = {N_ATTACK: (GUARD_CROUCH, 12), N_SPECIAL: (GUARD_M, 15)}
     for e in events[:3]:
-        assert e[3] in (GUARD_M, GUARD_STAND, GUARD_CROUCH) and e[4] in (12, 15) and e[5] == -0.3, e
-    assert broke_at is not None and events[3][4] == 30 and events[3][5] == 0.0, events
+        assert e[6] in row and (e[3], e[4]) == row[e[6]] and e[5] == -0.3, e
+    assert broke_at is not None and events[3][6] in row, events
+    assert (events[3][3], events[3][4], events[3][5]) == (row[events[3][6]][0], 30, 0.0), events
     assert saw_guard_break_action
     assert last is not None
 

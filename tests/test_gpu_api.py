@@ -388,8 +388,11 @@ def test_device_actions_and_stream_interop():
 
 
 def test_vector_env_surface():
+    from footsies_gym_amd import vector_env as ve
     from footsies_gym_amd.vector_env import FootsiesVectorEnv
+    tuned = ve._HEAP_RETAINED
     env = FootsiesVectorEnv(64, seed=0)
+    assert ve._HEAP_RETAINED == tuned  # the glibc tuning is opt-in (retain_host_heap=True)
     obs, info = env.reset(seed=42)
     assert obs["guard"].shape == (64, 2) and obs["guard"].dtype == np.int64
     assert (obs["position"][:, 0] == -2).all() and (info["frame"] == -1).all()
@@ -403,6 +406,9 @@ def test_vector_env_surface():
             total_eps += int(term.sum())
             i = int(np.nonzero(term)[0][0])
             assert info["final_observation"][i] is not None
+            # final_info holds the final observation's own rows (FE:379), read-only
+            fo, fi = info["final_observation"][i], info["final_info"][i]
+            assert all(fi[k] is fo[k] and not fo[k].flags.writeable for k in fo)
             assert info["frame"][i] == -1  # same-step auto-reset: obs is the new episode's state(-1)
             assert obs["move"][i].tolist() == [0, 0]
         assert env.observation_space.contains(obs)

@@ -1,0 +1,85 @@
+"""The kernels bench.py reports, held directly against the CPU oracle at the bench's own shapes.
+
+`bench.py` times `fs_step_n_packed` over HBM action rows written by `fs_hash_actions`: 65 536
+arenas, a warm-up launch, then consecutive launches of `--steps` ticks (the driver runs
+`--steps 20 --warmup 5`) or SURVEY §8(d)'s 1000-tick launches, the arenas' state carried in HBM
+from launch to launch.  The same rows, copied to the host, drive the oracle one tick at a time
+(`or_step`, OpenMP on the host); every packed record of the compared launches, unpacked by
+`simulator.unpack_trajectory`, must equal the oracle's outputs of that tick bit for bit (final
+records where the arena terminated), and the full canonical state must be equal at the end.
+
+Three actor configurations, one per kernel instance the bench's legs run:
+* external P2 (`k_step_n_packed<0, 0>`, the headline),
+* the in-kernel bot as P2 (`<0, 1>`, the C2 opponent leg `p2_bot_mode`),
+* P2 switched to the bot in every other arena (`<0, 3>`, kActors, the `actors_mode.mixed_p2` leg).
+
+Reference semantics: BC:201-220 (the Fight tick), FE:518-570 (step's outputs and auto-reset).
+"""
+import numpy as np
+import pytest
+
+from footsies_gym_amd import _abi
+from tests.parity_utils import compare_outputs, compare_states
+
+pytestmark = pytest.mark.gpu
+
+N = 65536
+SEED = 0x5EED
+KERNEL = {"external": "fsk::k_step_n_packed<0, 0>", "bot": "fsk::k_step_n_packed<0, 1>",
+          "mixed": "fsk::k_step_n_packed<0, 3>"}
+# (launch sizes, launches compared): the driver's shape (--warmup 5, then 20-tick regions) and
+# SURVEY 8(d)'s (a 200-tick warm-up, then 1000-tick launches); launches are indexed in order
+SHAPES = {"driver_20": ([5] + [20] * 10, "all"), "c3_1000": ([200, 1000, 1000], (0, 2))}
+
+
+def _pair(oracle_lib, actors):
+    from footsies_gym_amd.simulator import FootsiesSim
+    p2 = "bot" if actors == "bot" else "external"
+    sim = FootsiesSim(N, p2_mode=p2, seed=0, arena_base=0)
+    ora = oracle_lib.Oracle(N, p2_mode=_abi.FS_P2_BOT if p2 == "bot" else _abi.FS_P2_EXTERNAL, base_seed=0)
+    if actors == "mixed":  # set_opponent / P2_BOT on the even arenas, as the bench's mixed_p2 leg
+        mask = (np.arange(N) % 2 == 0).astype(np.uint8)
+        sim.set_p2_mode("bot", mask)
+        assert ora.set_p2_mode(_abi.FS_P2_BOT, mask) == 0
+    compare_states(ora.state(), sim.get_state(), step=-1)
+    return sim, ora
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("actors", ["external", "bot", "mixed"])
+def test_bench_kernel_matches_oracle_at_bench_shape(oracle_lib, actors, shape):
+    import torch
+    from footsies_gym_amd._lib import lib
+    from footsies_gym_amd.simulator import unpack_trajectory
+    launches, compared = SHAPES[shape]
+    total = sum(launches)
+    sim, ora = _pair(oracle_lib, actors)
+    ext = actors != "bot"
+    # the bench's inputs: the hashed stream written to HBM before timing
+    p1, p2 = sim.hash_actions(total, seed=SEED, t0=0, p2=ext)
+    torch.cuda.synchronize()
+    h1 = p1.cpu().numpy()
+    h2 = p2.cpu().numpy() if ext else None
+    biggest = max(launches)
+    kname = lib().fs_step_kernel(sim.handle, biggest, _abi.FS_KERNEL_PACKED).decode()
+    assert kname == KERNEL[actors], kname
+    traj = sim.alloc_packed_trajectory(biggest)
+    k, checked = 0, 0
+    for j, m in enumerate(launches):
+        sim.step_n_packed(m, p1[k:k + m], p2[k:k + m] if ext else None, trajectory=traj)
+        torch.cuda.synchronize()
+        check = compared == "all" or j in compared
+        for t in range(m):
+            exp = ora.step(h1[k + t], h2[k + t] if ext else None)
+            if check:  # tick t's records copied once, then unpacked on the host
+                rec = {key: (None if v is None else v[t].cpu().numpy()) for key, v in traj.items()}
+                row = {key: np.ascontiguousarray(v) for key, v in unpack_trajectory(rec).items()}
+                compare_outputs(exp, row, step=k + t)
+                checked += 1
+        k += m
+    assert k == total and checked == (total if compared == "all" else sum(launches[j] for j in compared))
+    compare_states(ora.state(), sim.get_state(), step=total)
+    out = ora.outputs()
+    assert out["terminated"].any()  # rounds end inside the compared launches (final records ran)
+    sim.close()
+    ora.close()

@@ -271,3 +271,22 @@ def test_split_bf16_eval_agrees_with_fp32_eval():
     torch.testing.assert_close(vs, v32, rtol=1e-4, atol=5e-5)
     torch.testing.assert_close(lps, lp32, rtol=1e-4, atol=5e-5)
     assert not torch.equal(vs, v32) or not torch.equal(lps, lp32)
+
+
+def test_eval_precision_override_is_the_fp32_path():
+    """PPOTrainer's critic values and fp32 old log-probs (the KL diagnostic's reference) come from
+    evaluate(precision="fp32") whatever the learner's precision: a split-bf16 learner
+    asked for fp32 gives the fp32 learner's values and log-probs bit for bit."""
+    import torch
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=7)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    n = 5000
+    x = (torch.rand((n, 8), generator=g, device="cuda") * 2 - 0.5).contiguous()
+    a = torch.randint(0, 8, (n,), generator=g, device="cuda").to(torch.uint8)
+    v32, lp32 = PPOGrad(actor, critic).evaluate(x, a, n)
+    split = PPOGrad(actor, critic, precision="split_bf16")
+    v, lp = split.evaluate(x, a, n, precision="fp32")
+    assert torch.equal(v, v32) and torch.equal(lp, lp32)
+    with pytest.raises(ValueError):
+        split.evaluate(x, a, n, precision="bf16")

@@ -72,6 +72,67 @@ def worker(rank, port, q):
     dist.destroy_process_group()
 
 
+BENCH_N, BENCH_LAUNCHES = 4096, [5] + [20] * 5 + [7]
+
+
+def bench_flow(n, arena_base):
+    """What bench.py does on each rank: FootsiesSim(arena_base = rank * N), the hashed rows of
+    its own global arenas written to HBM (fs_hash_actions), then consecutive fs_step_n_packed
+    launches into one reused packed trajectory.  Returns every launch's records and the state."""
+    import torch
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(n, device=0, p2_mode="external", seed=0, arena_base=arena_base)
+    total = sum(BENCH_LAUNCHES)
+    p1, p2 = sim.hash_actions(total, seed=0x5EED, t0=0)
+    traj = sim.alloc_packed_trajectory(max(BENCH_LAUNCHES))
+    recs, k = [], 0
+    for m in BENCH_LAUNCHES:
+        sim.step_n_packed(m, p1[k:k + m], p2[k:k + m], trajectory=traj)
+        torch.cuda.synchronize()
+        recs.append({key: v[:m].cpu().numpy() for key, v in traj.items()})
+        k += m
+    state = sim.get_state()
+    sim.close()
+    return recs, state
+
+
+def bench_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    recs, state = bench_flow(BENCH_N, rank * BENCH_N)
+    q.put({"rank": rank, "recs": recs, "state": state})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_bench_flow_match_unsharded():
+    """bench.py's per-rank flow (hashed rows keyed by global index, packed fused launches of the
+    driver's shape) on two ranks sharing cuda:0: the ranks' records and states, concatenated in
+    rank order, equal one unsharded 2N-arena handle's byte for byte (VERDICT r04 weak #5)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=bench_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(WORLD):
+        r = q.get(timeout=240)
+        got[r["rank"]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    recs, state = bench_flow(WORLD * BENCH_N, 0)
+    assert np.concatenate([got[r]["state"] for r in range(WORLD)]).tobytes() == state.tobytes()
+    for j, want in enumerate(recs):
+        for key, v in want.items():
+            shard = np.concatenate([got[r]["recs"][j][key] for r in range(WORLD)], axis=1)
+            assert shard.tobytes() == v.tobytes(), (j, key)
+    assert any(w["lanes"][..., 1, 12].any() for w in recs)  # rounds ended (final records written)
+
+
 def test_two_ranks_on_one_gpu_match_unsharded():
     import torch.multiprocessing as mp
     from footsies_gym_amd.parallel import unpack_outputs

@@ -275,9 +275,10 @@ def test_single_env_host_conversion_equals_batch_path():
         assert types(o1) == types(o2) and types(i1) == types(i2)
 
 
-def test_retain_host_heap_is_opt_out_and_idempotent():
+def test_retain_host_heap_is_idempotent_and_refusable():
     """vector_env.retain_host_heap (mallopt: keep freed blocks on glibc's heap so a numpy step's
-    arrays do not re-fault their pages) applies once per process and honours FOOTSIES_NO_MALLOPT."""
+    arrays do not re-fault their pages; opt-in, FootsiesVectorEnv(retain_host_heap=True)) applies
+    once per process and honours FOOTSIES_NO_MALLOPT."""
     import subprocess
     import sys
     code = ("import sys; sys.path.insert(0, %r); from footsies_gym_amd import vector_env as v; "
@@ -329,6 +330,7 @@ def test_native_host_conversion_equals_numpy(n, threads, monkeypatch):
         assert np.array_equal(fo["guard"], out["final_guard"][j].astype(np.int64))
         assert np.array_equal(fi["p2_action"], [bool(out["final_action"][j, 1] & b) for b in (1, 2, 4)])
         assert fi["frame"] == out["final_frame"][j] and fi["p1_hitstun"] == out["final_hitstun"][j, 0]
+        assert not fo["guard"].flags.writeable and not fo["position"].flags.writeable  # shared: read-only
         # the final info's observation entries are the final observation's own rows (FE:379's **obs)
         assert list(fi) == ["frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun", "guard", "move",
                             "move_frame", "position"]
@@ -397,3 +399,27 @@ def test_unpack_trajectory_layout():
         assert v[k].dtype == want.dtype and np.array_equal(v[k], want), k
     assert not v["truncated"].any() and np.array_equal(v["final_frame"], frame)
     assert "final_terminated" not in v and np.array_equal(v["final_position"], pos)
+
+
+def test_native_host_conversion_rejects_rows_outside_the_source():
+    """fs_host_convert checks every row index against the source's n_src rows (and n <= n_src
+    without rows) before a thread starts: FS_E_INVALID, nothing read past the buffers."""
+    import ctypes as C
+    from footsies_gym_amd import _abi
+    from footsies_gym_amd._lib import lib
+    n_src = 10
+    src = {k: np.zeros((n_src, 2) if k in ("guard", "move", "move_frame", "position", "action", "hitstun") else n_src,
+                       dt) for k, dt in (("guard", np.uint8), ("move", np.uint8), ("move_frame", np.float32),
+                                         ("position", np.float32), ("action", np.uint8), ("hitstun", np.uint8),
+                                         ("frame", np.int32))}
+    so = _abi.fs_outputs(**{k: v.ctypes.data for k, v in src.items()})
+    out = np.zeros((n_src, 2), np.int64)
+    dst = _abi.fs_host_arrays(guard=out.ctypes.data)
+    L = lib()
+    ok = np.array([0, 9, 3], np.int64)
+    assert L.fs_host_convert(C.byref(so), n_src, ok.ctypes.data, 3, C.byref(dst), 1) == _abi.FS_OK
+    for bad in ([0, 10], [-1], [3, 2**40]):
+        r = np.array(bad, np.int64)
+        assert L.fs_host_convert(C.byref(so), n_src, r.ctypes.data, len(r), C.byref(dst), 1) == _abi.FS_E_INVALID
+    assert L.fs_host_convert(C.byref(so), n_src, None, n_src + 1, C.byref(dst), 1) == _abi.FS_E_INVALID
+    assert L.fs_host_convert(C.byref(so), n_src, None, n_src, C.byref(dst), 1) == _abi.FS_OK
