@@ -13,8 +13,9 @@
 //
 // Semantics are exactly env_step's (fs_kernels.hip), phase by phase and in the same operation
 // order; the CPU oracle and the GPU parity suite hold both kernels to the same bits.  Used for
-// the fused launches with action rows (fs_step_n) and a remote, idle or bot P2; the one-tick,
-// hashed-action, policy and per-arena-actor launches keep the two-lane kernel.
+// the fused launches with action rows (fs_step_n, and fs_step_n_packed: k_step_n1_packed) and a
+// remote, idle or bot P2; the one-tick, hashed-action, policy and per-arena-actor launches keep
+// the two-lane kernel.
 //
 // Paths: BC = Assets/Script/BattleCore.cs, F = Assets/Script/Fighter.cs, AI = Assets/Script/BattleAI.cs,
 // FE = footsies-gym/footsies_gym/envs/footsies.py.
@@ -289,6 +290,23 @@ __device__ __forceinline__ void write_final1(const Arena1& A, const DevOutputs& 
              o.final_hitstun, r);
 }
 
+// fs_step_n_packed: the two lane records of the arena (include/footsies.h fs_packed_traj, the
+// layout packed_record writes from the two-lane kernel) at records 2 r and 2 r + 1, as two 16-B
+// stores; w3 of P1's record is the frame, of P2's the terminated byte (0 in a final record).
+__device__ __forceinline__ PkRec packed_record1(const Fighter& f, uint32_t rec_count, uint32_t rec, uint32_t w3) {
+  PkRec v;
+  const uint32_t act = rec_count > 0 ? rec : 0u;  // a 3-bit input
+  v.x = (uint32_t)f.guard | (obs_move(f) << 8) | (act << 16) | ((uint32_t)f.stun << 24);
+  v.y = __float_as_uint(obs_move_frame(f));
+  v.z = __float_as_uint(f.x);
+  v.w = w3;
+  return v;
+}
+__device__ __forceinline__ void write_packed1(const Arena1& A, uint4* base, uint32_t r, uint32_t w3_p2) {
+  st_off(reinterpret_cast<PkRec*>(base), 32u * r, packed_record1(A.f0, A.rec_count, A.rec0, (uint32_t)A.frame_count));
+  st_off(reinterpret_cast<PkRec*>(base), 32u * r + 16u, packed_record1(A.f1, A.rec_count, A.rec1, w3_p2));
+}
+
 // (see opaque_burst_results)
 __device__ __forceinline__ void opaque_burst_results1(Arena1& A) {
   asm volatile("" : "+v"(A.f0.x), "+v"(A.f0.act), "+v"(A.f0.frame), "+v"(A.f0.vital), "+v"(A.f0.guard),
@@ -311,7 +329,7 @@ __device__ __forceinline__ void settle2(uint32_t& n1, uint32_t& n2) {
 }
 
 // one env-step of one arena: env_step's phases for both fighters
-template <int FM, int P2, int WAIT>
+template <int FM, int P2, int WAIT, bool PK>
 __device__ __forceinline__ void env_step1(Arena1& A, uint32_t a1, uint32_t a2, const StepParams& p, uint32_t r,
                                           uint32_t& n1, uint32_t& n2) {
   constexpr bool BOT = P2 == FS_P2_BOT;
@@ -323,10 +341,15 @@ __device__ __forceinline__ void env_step1(Arena1& A, uint32_t a1, uint32_t a2, c
     A.cum = 0.0;
     A.ai0 = A.ai1 = stand_info();
     settle2<WAIT>(n1, n2);
-    write_main1(A, o, r);
-    st_off(o.reward, 8 * r, 0.0);
-    st_off(o.terminated, r, (uint8_t)0);
-    st_off(o.truncated, r, (uint8_t)0);
+    if constexpr (PK) {
+      write_packed1(A, o.pk_lanes, r, 0u);
+      st_off(o.reward, 8 * r, 0.0);
+    } else {
+      write_main1(A, o, r);
+      st_off(o.reward, 8 * r, 0.0);
+      st_off(o.terminated, r, (uint8_t)0);
+      st_off(o.truncated, r, (uint8_t)0);
+    }
     opaque_burst_results1(A);
     return;
   }
@@ -404,7 +427,8 @@ __device__ __forceinline__ void env_step1(Arena1& A, uint32_t a1, uint32_t a2, c
     A.f0.hist = A.f1.hist = 0;  // ChangeRoundState(KO): ClearInput (BC:296-299)
     A.f0.hold = A.f1.hold = 0;
     if (p.autoreset_mode == FS_AUTORESET_SAME_STEP) {
-      write_final1(A, o, r);
+      if constexpr (PK) write_packed1(A, o.pk_final, r, 0u);
+      else write_final1(A, o, r);
       reset_burst1<FM, P2>(A, true);
       A.cum = 0.0;
       A.has_term = 0;
@@ -418,10 +442,15 @@ __device__ __forceinline__ void env_step1(Arena1& A, uint32_t a1, uint32_t a2, c
       A.bin = bot_next_input1(A.bot, bot_distance<FM>(A.f0.x, A.f1.x), (uint32_t)A.f0.act, bpre);
     A.has_term = 0;
   }
-  write_main1(A, o, r);
-  st_off(o.reward, 8 * r, reward);
-  st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
-  st_off(o.truncated, r, (uint8_t)0);
+  if constexpr (PK) {
+    write_packed1(A, o.pk_lanes, r, over ? 1u : 0u);
+    st_off(o.reward, 8 * r, reward);
+  } else {
+    write_main1(A, o, r);
+    st_off(o.reward, 8 * r, reward);
+    st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
+    st_off(o.truncated, r, (uint8_t)0);
+  }
   asm volatile("" ::"v"(A.ai0), "v"(A.ai1));
 }
 
@@ -429,15 +458,16 @@ __device__ __forceinline__ void env_step1(Arena1& A, uint32_t a1, uint32_t a2, c
 // tick t (two untracked loads into the slot of tick t's rows, D slots in all), and before tick t's
 // stores the wave waits for tick t + 1's rows with vmcnt(12 (D - 1)): ticks t + 1 - D .. t - 1 issued
 // 10 output stores and 2 row loads each after them (tools/check_async_loads.py proves the count on
-// the assembly).  Loads and stores retire in order on gfx9, so that wait also needs the stores of
+// the assembly).  Packed trajectories (PK): 3 stores per tick (the two lane records and the
+// reward), so vmcnt(5 (D - 1)).  Loads and stores retire in order on gfx9, so that wait also needs the stores of
 // tick t - D to be acknowledged: a deeper pipeline asks for older stores only.
 #ifndef FS_ROW_DEPTH
 #define FS_ROW_DEPTH 3
 #endif
-template <int FM, int P2>
+template <int FM, int P2, bool PK>
 __device__ __forceinline__ void step_body1(const StepParams& p) {
   constexpr int D = FS_ROW_DEPTH;
-  constexpr int W = 12 * (D - 1);
+  constexpr int W = (PK ? 5 : 12) * (D - 1);
   // (the main loop below unrolls at most four ticks per iteration and the remainder handles at most
   // three, so a deeper pipeline would skip ticks; vmcnt's 6-bit field bounds W as well)
   static_assert(D >= 2 && D <= 4 && W <= 63, "row pipeline depth 2..4");
@@ -484,7 +514,7 @@ __device__ __forceinline__ void step_body1(const StepParams& p) {
     fl1[j] = issue1(t + D);
     fl2[j] = issue2(t + D);
     uint32_t n1 = fl1[jn], n2 = fl2[jn];
-    env_step1<FM, P2, W>(A, rd1 & 7u, rd2 & 7u, p, (uint32_t)t * row_step + (uint32_t)a, n1, n2);
+    env_step1<FM, P2, W, PK>(A, rd1 & 7u, rd2 & 7u, p, (uint32_t)t * row_step + (uint32_t)a, n1, n2);
     rd1 = n1;
     rd2 = n2;
   };
@@ -513,5 +543,11 @@ __device__ __forceinline__ void step_body1(const StepParams& p) {
 
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n1(StepParams p) {
-  step_body1<FM, P2>(p);
+  step_body1<FM, P2, false>(p);
+}
+
+// fs_step_n_packed with one lane per arena (the launches k_step_n1 takes, packed records)
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step_n1_packed(StepParams p) {
+  step_body1<FM, P2, true>(p);
 }

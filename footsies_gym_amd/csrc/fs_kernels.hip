@@ -2115,7 +2115,15 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   StepParams p = p_in;
   p.prio = two_waves_per_simd(p.n_envs);
   if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
-  else if (p.out.pk_lanes) hipLaunchKernelGGL((k_step_n_packed<FM, P2>), grid, block, 0, s, p);  // (rows: fs_api checks)
+  else if (p.out.pk_lanes) {  // (rows: fs_api checks)
+    if constexpr (P2 != kActors) {
+      if (!p.geom && fused_one_lane(p.n_envs)) {
+        hipLaunchKernelGGL((k_step_n1_packed<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_step_n_packed<FM, P2>), grid, block, 0, s, p);
+  }
   else if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
   else if constexpr (P2 != kActors) {
@@ -2147,8 +2155,9 @@ hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStre
 const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant, bool geom,
                              bool packed) {
   static thread_local char buf[64];
-  const char* k = policy ? "k_step_n_policy" : packed ? "k_step_n_packed" : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step"
-                : (variant != kActors && !geom && fused_one_lane(n_envs)) ? "k_step_n1" : "k_step_n";
+  const bool one = !policy && !hashed && variant != kActors && !geom && fused_one_lane(n_envs);
+  const char* k = policy ? "k_step_n_policy" : packed ? (one ? "k_step_n1_packed" : "k_step_n_packed")
+                : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step" : one ? "k_step_n1" : "k_step_n";
   snprintf(buf, sizeof buf, "fsk::%s<%d, %d>", k, float_mode == FS_FLOAT_DOUBLE ? 1 : 0, variant);
   return buf;
 }

@@ -56,6 +56,45 @@ def test_one_lane_kernel_at_its_size(oracle_lib, p2):
     fused_vs_oracle(oracle_lib, 131072, 41, p2, seed=6)
 
 
+def packed_vs_oracle(oracle_lib, N, launches, p2, seed=5):
+    """fs_step_n_packed launches of the given tick counts over device rows into one packed
+    trajectory; every record of every launch (unpacked) and the final state against the oracle."""
+    import torch
+    from footsies_gym_amd._lib import lib
+    from footsies_gym_amd.simulator import FootsiesSim, unpack_trajectory
+    sim = FootsiesSim(N, p2_mode=p2, seed=seed)
+    ora = oracle_lib.Oracle(N, p2_mode=P2[p2], base_seed=seed)
+    ext = p2 == "external"
+    traj = sim.alloc_packed_trajectory(max(launches))
+    k = 0
+    for c, T in enumerate(launches):
+        p1, p2a = sim.hash_actions(T, seed=0xB7, t0=k, p2=ext)
+        sim.step_n_packed(T, p1, p2a if ext else None, trajectory=traj)
+        torch.cuda.synchronize()
+        h1, h2 = p1.cpu().numpy(), (p2a.cpu().numpy() if ext else None)
+        for t in range(T):
+            exp = ora.step(h1[t], None if h2 is None else h2[t])
+            rec = {key: (None if v is None else v[t].cpu().numpy()) for key, v in traj.items()}
+            compare_outputs(exp, {key: np.ascontiguousarray(v) for key, v in unpack_trajectory(rec).items()}, step=k + t)
+        k += T
+    compare_states(ora.state(), sim.get_state(), step=k)
+    name = lib().fs_step_kernel(sim.handle, max(launches), _abi.FS_KERNEL_PACKED).decode()
+    sim.close()
+    return name
+
+
+@pytest.mark.parametrize("N", [131072, 262144])
+@pytest.mark.parametrize("p2", ["external", "bot"])
+def test_one_lane_packed_kernel_at_its_sizes(oracle_lib, N, p2):
+    """fs_step_n_packed at C4's one- and two-GPU strong-scaling shapes (262 144 and 131 072 arenas
+    per GPU) runs the one-lane packed kernel (k_step_n1_packed); its records against the oracle,
+    an even launch then an odd one (the row pipeline's tail)."""
+    if os.environ.get("FOOTSIES_FUSED_LANES") == "2":
+        pytest.skip("the two-lane kernel is forced")
+    name = packed_vs_oracle(oracle_lib, N, [24, 17], p2)
+    assert name == "fsk::k_step_n1_packed<0, %d>" % P2[p2], name
+
+
 @pytest.mark.parametrize("p2", ["external", "bot", "noop"])
 @pytest.mark.parametrize("fm,ar,dense", [("strict", "same_step", True), ("double", "same_step", True),
                                          ("strict", "next_step", True), ("double", "next_step", False),
@@ -68,16 +107,19 @@ def test_modes_fused(oracle_lib, p2, fm, ar, dense):
 
 
 def test_fused_tests_with_the_one_lane_kernel_forced():
-    """This file's mode tests and test_gpu_api.py's fused tests (trajectory vs single steps,
+    """This file's mode tests, test_gpu_api.py's fused tests (trajectory vs single steps,
     ragged 1 / 33 / 97-arena grids and odd tick counts, frame_delay, launches split by the
-    32-bit offset limit) in one child process with FOOTSIES_FUSED_LANES=1."""
+    32-bit offset limit) and test_gpu_packed.py's packed-vs-per-field twins (so the one-lane
+    packed kernel meets the one-lane per-field one on every mode) in one child process with
+    FOOTSIES_FUSED_LANES=1."""
     if os.environ.get("FOOTSIES_FUSED_LANES"):
         pytest.skip("already the child")
     env = dict(os.environ, FOOTSIES_FUSED_LANES="1")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
                         os.path.join(ROOT, "tests", "test_gpu_one_lane.py") + "::test_modes_fused",
-                        os.path.join(ROOT, "tests", "test_gpu_api.py"), "-k",
-                        "test_modes_fused or step_n_trajectory or fused_ragged or frame_delay_paths or long_fused"],
+                        os.path.join(ROOT, "tests", "test_gpu_api.py"), os.path.join(ROOT, "tests", "test_gpu_packed.py"),
+                        "-k", "test_modes_fused or step_n_trajectory or fused_ragged or frame_delay_paths or long_fused "
+                              "or packed_trajectory"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert " passed" in r.stdout and " failed" not in r.stdout, r.stdout[-2000:]

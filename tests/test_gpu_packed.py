@@ -3,6 +3,8 @@ f64 reward, include/footsies.h fs_packed_traj) instead of one array per field.  
 through simulator.unpack_trajectory's strided views, must equal the fs_step_n trajectory of a twin
 handle on the same state and actions, byte for byte (the per-field path is itself held to the
 oracle by test_gpu_parity / test_gpu_api), and the two handles must end in the same state."""
+import os
+
 import numpy as np
 import pytest
 
@@ -114,7 +116,9 @@ def test_packed_trajectory_argument_errors():
     with pytest.raises(FootsiesError):  # the delayed queue reads the per-field outputs
         delayed.step_n_packed(4, p1, q2)
     from footsies_gym_amd._lib import lib  # the kernel a packed call runs, as rocprofv3 names it
-    assert lib().fs_step_kernel(sim.handle, 4, _abi.FS_KERNEL_PACKED).decode() == "fsk::k_step_n_packed<0, 0>"
+    one = os.environ.get("FOOTSIES_FUSED_LANES") == "1"  # (test_gpu_one_lane.py's child forces the one-lane kernel)
+    assert lib().fs_step_kernel(sim.handle, 4, _abi.FS_KERNEL_PACKED).decode() == (
+        "fsk::k_step_n1_packed<0, 0>" if one else "fsk::k_step_n_packed<0, 0>")
     torch.cuda.synchronize()
 
 

@@ -44,6 +44,7 @@ def test_no_kernel_uses_scratch(src):
     if src == "fs_kernels.hip":
         # every template instance of the step kernels is present, the per-arena-actor ones included
         names = " ".join(res)
-        for k in ("k_step_n", "k_step", "k_step_n_policy", "k_step_n_hashed", "k_step_n1", "k_reset"):
+        for k in ("k_step_n", "k_step", "k_step_n_policy", "k_step_n_hashed", "k_step_n1", "k_step_n1_packed",
+                  "k_step_n_packed", "k_reset"):
             assert re.search(r"\b_ZN3fsk\d+%sI" % k, names), k
         assert sum("ILi0ELi3EE" in n or "ILi1ELi3EE" in n for n in res) >= 8  # kActors = 3
