@@ -464,9 +464,12 @@ __device__ __forceinline__ void env_step1(Arena1& A, uint32_t a1, uint32_t a2, c
 #ifndef FS_ROW_DEPTH
 #define FS_ROW_DEPTH 3
 #endif
+#ifndef FS_ROW_DEPTH_PK
+#define FS_ROW_DEPTH_PK FS_ROW_DEPTH
+#endif
 template <int FM, int P2, bool PK>
 __device__ __forceinline__ void step_body1(const StepParams& p) {
-  constexpr int D = FS_ROW_DEPTH;
+  constexpr int D = PK ? FS_ROW_DEPTH_PK : FS_ROW_DEPTH;
   constexpr int W = (PK ? 5 : 12) * (D - 1);
   // (the main loop below unrolls at most four ticks per iteration and the remainder handles at most
   // three, so a deeper pipeline would skip ticks; vmcnt's 6-bit field bounds W as well)

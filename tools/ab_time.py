@@ -5,8 +5,8 @@
 
 Each library is timed in its own subprocess (FOOTSIES_LIB override), rounds interleaved so
 box-level drift hits every variant alike.  Per library and P2 mode (external = C3, bot = C2):
-the median duration of back-to-back fs_step_n launches of T ticks over N arenas with full
-trajectories, bracketed by HIP events on the launch stream.
+the median duration of back-to-back fs_step_n launches (fs_step_n_packed with --packed) of T
+ticks over N arenas with full trajectories, bracketed by HIP events on the launch stream.
 """
 import argparse
 import os
@@ -26,11 +26,18 @@ res = []
 for mode in ("external", "bot"):
     sim = FootsiesSim(N, p2_mode=mode, seed=0)
     p1, p2 = sim.hash_actions(T, seed=0x5EED, p2=(mode == "external"))
-    traj = sim.alloc_trajectory(T)
-    td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
     q2 = C.c_void_p(p2.data_ptr()) if mode == "external" else None
-    def run():
-        check(lib().fs_step_n(sim.handle, T, C.c_void_p(p1.data_ptr()), q2, 0, C.byref(td)), sim.handle)
+    if %(packed)d:  # fs_step_n_packed into packed records (the bench's layout)
+        traj = sim.alloc_packed_trajectory(T)
+        td = _abi.fs_packed_traj(lanes=traj["lanes"].data_ptr(), reward=traj["reward"].data_ptr(),
+                                 final_lanes=traj["final_lanes"].data_ptr())
+        def run():
+            check(lib().fs_step_n_packed(sim.handle, T, C.c_void_p(p1.data_ptr()), q2, C.byref(td)), sim.handle)
+    else:
+        traj = sim.alloc_trajectory(T)
+        td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+        def run():
+            check(lib().fs_step_n(sim.handle, T, C.c_void_p(p1.data_ptr()), q2, 0, C.byref(td)), sim.handle)
     run(); torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
     torch.cuda._sleep(int(2e7))
@@ -68,8 +75,9 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--ticks", type=int, default=1000)
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--packed", action="store_true", help="time fs_step_n_packed (the bench's layout)")
     a = ap.parse_args()
-    code = CODE % dict(root=ROOT, envs=a.envs, ticks=a.ticks, launches=a.launches)
+    code = CODE % dict(root=ROOT, envs=a.envs, ticks=a.ticks, launches=a.launches, packed=int(a.packed))
     times = {lib: [] for lib in a.libs}
     for r in range(a.rounds):
         for lib in a.libs:
