@@ -92,6 +92,7 @@ struct StepParams {
   int p2_noop;    // kActors: a non-bot P2 presses nothing (FS_P2_NOOP handle)
   int prio;       // fused launches: time-sliced wave priority (set by the launcher, prio_slice)
   int geom;       // some arena has position.y != 0 or a flipped facing: the general-geometry tick
+  int prefetch;   // two-lane fused row launches: each tick's request prepared at the end of the tick before
   // host actions of a one-tick launch over at most kInlineArenas arenas, carried in the kernel
   // arguments instead of a staging copy (inl_n != 0): byte a of inl[player] is arena a's input
   int inl_n;

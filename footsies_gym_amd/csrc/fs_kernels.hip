@@ -1403,8 +1403,40 @@ __device__ __forceinline__ void opaque_burst_results(Lane& L) {
                "+v"(L.rec_count));
 }
 
-template <int FM, int P2, int WAIT = -1, int TP = kTabLds, bool GEOM = false, bool PK = false>
-__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next) {
+// Tick t + 1's request inputs, prepared at the end of tick t (the fused row loop at one wave per
+// SIMD, StepParams::prefetch): UpdateInput (F:172-188) and IncrementActionFrame (F:140-166) of tick
+// t + 1 depend only on its input -- resident once tick t has waited for the next row -- and on the
+// fighter after tick t, so they run after tick t's stores, and the request-table entry and the
+// continuing frame record are read then: the next tick's head starts with both resident instead of
+// waiting for that dependent LDS round trip (a lone wave has no partner to issue in the wait).
+// The C# order of tick t + 1 is unchanged: nothing between the end of tick t and UpdateInput of
+// tick t + 1 (frameCount++, RecordInput) reads or writes what these phases touch.
+struct Pre {
+  InputEval e;
+  uint32_t q;      // request-table entry (kTables.req_table[request_sel])
+  int rec_cont;    // frame record if the action continues
+  uint32_t keep;   // hasWon / an early return (request_sel's `keep`)
+};
+// The input a tick of this lane acts on, from its action row's byte (env_step's `in`, not stored)
+template <int P2>
+__device__ __forceinline__ uint32_t tick_input(const Lane& L, uint32_t a_own) {
+  static_assert(P2 != kActors, "(the per-arena actors take env_step's own path)");
+  if (L.k == 0 || P2 == FS_P2_EXTERNAL) return a_own;
+  return P2 == FS_P2_BOT ? L.bin : 0u;
+}
+__device__ __forceinline__ void prepare_request(Lane& L, uint32_t in, Pre& pre) {
+  pre.e = update_input(L.f, in, L.k ? kRelLut1 : kRelLut0);
+  increment_action_frame(L.f, L.ai);
+  pre.rec_cont = frame_record<false>(L.f);
+  bool keep;
+  const uint32_t sel = request_sel(L.f, pre.e, L.ai, keep);
+  pre.keep = keep;
+  pre.q = sT.req_table[sel];
+}
+
+template <int FM, int P2, int WAIT = -1, int TP = kTabLds, bool GEOM = false, bool PK = false, bool PF = false>
+__device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepParams& p, uint32_t r, uint32_t& next,
+                                         const Pre& pre = Pre{}, bool use_pre = false) {
   constexpr bool BOT = P2 == FS_P2_BOT;
   constexpr bool G = TP == kTabGlobal;  // the tables from global memory: a one-tick launch (k_step),
                                         // where no next tick reads L.ai
@@ -1456,14 +1488,23 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
   }
   // the fighter's facing: the player's own, or flipped by a state load (general geometry)
   const uint32_t face = GEOM ? k ^ L.f.flip : k;
-  const InputEval e = update_input(L.f, in, face ? kRelLut1 : kRelLut0);
-  const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
-  increment_action_frame(L.f, ai);
-  // the record if the action continues, read alongside the request entry; a
-  // request that sets an action returns that action's frame-0 record
-  const int rec_cont = frame_record<G>(L.f);
+  InputEval e;
+  int rec_cont;
   uint32_t rec_set;
-  const bool set = update_action_request<G>(L.f, e, ai, &rec_set);
+  bool set;
+  if (PF && use_pre) {  // prepared at the end of the previous tick (prepare_request; uniform per wave)
+    e = pre.e;
+    rec_cont = pre.rec_cont;
+    set = apply_request(L.f, pre.q, pre.keep != 0, e, &rec_set);
+  } else {
+    e = update_input(L.f, in, face ? kRelLut1 : kRelLut0);
+    const AInfo ai = L.ai;  // ActionInfo of f.act, re-read at the end of the previous tick
+    increment_action_frame(L.f, ai);
+    // the record if the action continues, read alongside the request entry; a
+    // request that sets an action returns that action's frame-0 record
+    rec_cont = frame_record<G>(L.f);
+    set = update_action_request<G>(L.f, e, ai, &rec_set);
+  }
   L.f.rec = set ? (int)rec_set : rec_cont;
   // One LDS round trip for everything the rest of the tick reads from the tables: my frame
   // record, the y half of the box-pair overlaps (records only, kTables.ybits) and the hit
@@ -1588,9 +1629,10 @@ __device__ __forceinline__ void policy_features(const Lane& L, uint32_t& d0, uin
 // POL samples P1's action every tick from the MLP actor (fs_policy.h); its MFMAs and lane
 // exchanges need the whole wave, so lanes past the last arena stay in the loop (on a copy
 // of arena 0 that they never store) unless their whole wave is idle.
-template <int FM, int P2, bool FUSED, bool HASH, bool POL = false, bool GEOM = false, bool PK = false>
+template <int FM, int P2, bool FUSED, bool HASH, bool POL = false, bool GEOM = false, bool PK = false, bool PF = false>
 __device__ __forceinline__ void step_body(const StepParams& p) {
   static_assert(!PK || (FUSED && !HASH && !POL), "packed trajectories: the fused row loop only");
+  static_assert(!PF || (FUSED && !HASH && !POL && !GEOM && P2 != kActors), "request prefetch: the standard row loop");
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = l < 2 * p.n_envs;
   const int a = active ? l >> 1 : 0;
@@ -1685,23 +1727,35 @@ __device__ __forceinline__ void step_body(const StepParams& p) {
       asm volatile("s_waitcnt vmcnt(0)\n\tv_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(a_rd), "=v"(b_rd)
                    : "v"(a_fl), "v"(b_fl) : "memory");
       const uint32_t grp = prio_group();
+      // PF: each tick but the launch's first starts from the request prepared at the end of the
+      // tick before it (prepare_request), from the row that tick made resident
+      Pre pre{};
+      bool have = false;
       int t = 0;
       for (; t < last; t += 2) {
         a_fl = issue(t + 2);
         if (p.prio) prio_slice(grp);
-        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a, b_fl);
+        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK, PF>(L, reads ? a_rd & 7u : 0u, p,
+                                                        (uint32_t)t * row_step + (uint32_t)a, b_fl, pre, have);
         b_rd = b_fl;
+        if constexpr (PF) {
+          prepare_request(L, tick_input<P2>(L, reads ? b_rd & 7u : 0u), pre);
+          have = true;
+        }
         b_fl = issue(t + 3);
         if (p.prio) prio_slice(grp);
-        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK>(L, reads ? b_rd & 7u : 0u, p,
-                                                (uint32_t)(t + 1) * row_step + (uint32_t)a, a_fl);
+        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK, PF>(L, reads ? b_rd & 7u : 0u, p,
+                                                        (uint32_t)(t + 1) * row_step + (uint32_t)a, a_fl, pre, PF);
         a_rd = a_fl;
+        if constexpr (PF) {
+          if (t + 2 <= last) prepare_request(L, tick_input<P2>(L, reads ? a_rd & 7u : 0u), pre);
+        }
       }
       if (t == last) {  // an odd tick count: the last tick waits for a re-read of the last row
         a_fl = issue(t + 2);
         uint32_t b_last = b_fl;  // (b_fl itself stays the in-flight value for the final wait)
-        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK>(L, reads ? a_rd & 7u : 0u, p, (uint32_t)t * row_step + (uint32_t)a,
-                                                b_last);
+        env_step<FM, P2, kRowWait, kTabLds, GEOM, PK, PF>(L, reads ? a_rd & 7u : 0u, p,
+                                                        (uint32_t)t * row_step + (uint32_t)a, b_last, pre, have);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::"v"(a_fl), "v"(b_fl) : "memory");  // no load outlives the wave
     }
@@ -1789,15 +1843,33 @@ __global__ __launch_bounds__(256) void k_step(StepParams p) {
 // uniform over the launch) as two loops: the standard loop carries none of the y state.
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n(StepParams p) {
-  if (p.geom) step_body<FM, P2, true, false, false, true>(p);
-  else step_body<FM, P2, true, false>(p);
+  if (p.geom) {
+    step_body<FM, P2, true, false, false, true>(p);
+    return;
+  }
+  if constexpr (P2 != kActors) {
+    if (p.prefetch) {
+      step_body<FM, P2, true, false, false, false, false, true>(p);
+      return;
+    }
+  }
+  step_body<FM, P2, true, false>(p);
 }
 
 // fs_step_n_packed: the row loop of k_step_n storing packed trajectory records
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n_packed(StepParams p) {
-  if (p.geom) step_body<FM, P2, true, false, false, true, true>(p);
-  else step_body<FM, P2, true, false, false, false, true>(p);
+  if (p.geom) {
+    step_body<FM, P2, true, false, false, true, true>(p);
+    return;
+  }
+  if constexpr (P2 != kActors) {
+    if (p.prefetch) {
+      step_body<FM, P2, true, false, false, false, true, true>(p);
+      return;
+    }
+  }
+  step_body<FM, P2, true, false, false, false, true>(p);
 }
 
 template <int FM, int P2>
@@ -2109,11 +2181,26 @@ static bool two_waves_per_simd(int n_envs) {
   return (2 * (int64_t)n_envs + 63) / 64 > simds;
 }
 
+// Whether a two-lane fused row launch prepares each tick's request at the end of the tick before
+// (Pre / prepare_request): at one wave per SIMD, where no partner wave issues in that LDS wait
+// (DESIGN.md section 5); same-step auto-reset only (no tick is a next-step reset burst).
+// FOOTSIES_PREFETCH=0 / 1 forces it off / on (A/B timing, and the parity suite runs both).
+static bool request_prefetch(const StepParams& p) {
+  static const int forced = [] {
+    const char* e = getenv("FOOTSIES_PREFETCH");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' + 1 : 0;
+  }();
+  if (p.autoreset_mode != FS_AUTORESET_SAME_STEP || p.geom || p.pol.w1 || !p.p1 || p.n_steps < 2) return false;
+  if (forced) return forced == 2;
+  return !two_waves_per_simd(p.n_envs);
+}
+
 template <int FM, int P2>
 static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   const dim3 grid = grid_for(2 * p_in.n_envs), block(kBlock);
   StepParams p = p_in;
   p.prio = two_waves_per_simd(p.n_envs);
+  p.prefetch = P2 != kActors && request_prefetch(p);
   if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
   else if (p.out.pk_lanes) {  // (rows: fs_api checks)
     if constexpr (P2 != kActors) {

@@ -15,6 +15,10 @@ Three actor configurations, one per kernel instance the bench's legs run:
 
 Reference semantics: BC:201-220 (the Fight tick), FE:518-570 (step's outputs and auto-reset).
 """
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -25,6 +29,7 @@ pytestmark = pytest.mark.gpu
 
 N = 65536
 SEED = 0x5EED
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = {"external": "fsk::k_step_n_packed<0, 0>", "bot": "fsk::k_step_n_packed<0, 1>",
           "mixed": "fsk::k_step_n_packed<0, 3>"}
 # (launch sizes, launches compared): the driver's shape (--warmup 5, then 20-tick regions) and
@@ -32,13 +37,13 @@ KERNEL = {"external": "fsk::k_step_n_packed<0, 0>", "bot": "fsk::k_step_n_packed
 SHAPES = {"driver_20": ([5] + [20] * 10, "all"), "c3_1000": ([200, 1000, 1000], (0, 2))}
 
 
-def _pair(oracle_lib, actors):
+def _pair(oracle_lib, actors, n=N):
     from footsies_gym_amd.simulator import FootsiesSim
     p2 = "bot" if actors == "bot" else "external"
-    sim = FootsiesSim(N, p2_mode=p2, seed=0, arena_base=0)
-    ora = oracle_lib.Oracle(N, p2_mode=_abi.FS_P2_BOT if p2 == "bot" else _abi.FS_P2_EXTERNAL, base_seed=0)
+    sim = FootsiesSim(n, p2_mode=p2, seed=0, arena_base=0)
+    ora = oracle_lib.Oracle(n, p2_mode=_abi.FS_P2_BOT if p2 == "bot" else _abi.FS_P2_EXTERNAL, base_seed=0)
     if actors == "mixed":  # set_opponent / P2_BOT on the even arenas, as the bench's mixed_p2 leg
-        mask = (np.arange(N) % 2 == 0).astype(np.uint8)
+        mask = (np.arange(n) % 2 == 0).astype(np.uint8)
         sim.set_p2_mode("bot", mask)
         assert ora.set_p2_mode(_abi.FS_P2_BOT, mask) == 0
     compare_states(ora.state(), sim.get_state(), step=-1)
@@ -48,12 +53,45 @@ def _pair(oracle_lib, actors):
 @pytest.mark.parametrize("shape", sorted(SHAPES))
 @pytest.mark.parametrize("actors", ["external", "bot", "mixed"])
 def test_bench_kernel_matches_oracle_at_bench_shape(oracle_lib, actors, shape):
+    run_shape(oracle_lib, actors, shape, N)
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("actors", ["external", "bot"])
+def test_c4_per_gpu_shape_matches_oracle(oracle_lib, actors, shape):
+    """C4's per-GPU shape (262 144 arenas over 8 GPUs: 32 768 per GPU, one wave per SIMD), where
+    the two-lane fused launches prepare each tick's request at the end of the tick before
+    (StepParams::prefetch): the same bench shapes against the oracle."""
+    run_shape(oracle_lib, actors, shape, 32768)
+
+
+def test_prefetch_forced_on_the_fused_suites():
+    """The request prefetch (prepare_request) forced on every two-lane fused row launch
+    (FOOTSIES_PREFETCH=1) in a child process: this file's 65 536-arena bench shapes, the packed
+    twins of test_gpu_packed.py and the fused tests of test_gpu_api.py / test_gpu_one_lane.py (every
+    float model, reward kind and P2 kind; next-step auto-reset launches keep the plain loop)."""
+    if os.environ.get("FOOTSIES_PREFETCH"):
+        pytest.skip("already the child")
+    env = dict(os.environ, FOOTSIES_PREFETCH="1", FOOTSIES_FUSED_LANES="2")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_gpu_bench_shapes.py") + "::test_bench_kernel_matches_oracle_at_bench_shape",
+                        os.path.join(ROOT, "tests", "test_gpu_packed.py"),
+                        os.path.join(ROOT, "tests", "test_gpu_one_lane.py") + "::test_modes_fused",
+                        os.path.join(ROOT, "tests", "test_gpu_api.py"), "-k",
+                        "bench_shape or packed_trajectory or test_modes_fused or step_n_trajectory or fused_ragged "
+                        "or frame_delay_paths or long_fused"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout and " failed" not in r.stdout, r.stdout[-2000:]
+
+
+def run_shape(oracle_lib, actors, shape, n):
     import torch
     from footsies_gym_amd._lib import lib
     from footsies_gym_amd.simulator import unpack_trajectory
     launches, compared = SHAPES[shape]
     total = sum(launches)
-    sim, ora = _pair(oracle_lib, actors)
+    sim, ora = _pair(oracle_lib, actors, n)
     ext = actors != "bot"
     # the bench's inputs: the hashed stream written to HBM before timing
     p1, p2 = sim.hash_actions(total, seed=SEED, t0=0, p2=ext)
@@ -62,7 +100,7 @@ def test_bench_kernel_matches_oracle_at_bench_shape(oracle_lib, actors, shape):
     h2 = p2.cpu().numpy() if ext else None
     biggest = max(launches)
     kname = lib().fs_step_kernel(sim.handle, biggest, _abi.FS_KERNEL_PACKED).decode()
-    assert kname == KERNEL[actors], kname
+    assert kname == KERNEL[actors] or os.environ.get("FOOTSIES_FUSED_LANES") == "1", kname
     traj = sim.alloc_packed_trajectory(biggest)
     k, checked = 0, 0
     for j, m in enumerate(launches):

@@ -81,7 +81,8 @@ ENV_STEP_MARKS = [
     ("settle_w<WAIT>(next);\n  if (over) {", "action rows: wait for the next tick's row (TrainingRemoteActor input)"),
     ("ChangeRoundState(KO)", "KO -> End -> Intro -> Fight burst (BC:212-345) [rare]"),
     ("TrainingManager.Step -> RequestNextInput", "BattleAI (AI:41-403)"),
-    ("write_main(L, o, r);\n  st_off(o.reward", "outputs: EnvironmentState / obs / info (BC:449-468, FE:336-380)"),
+    ("if constexpr (PK) {\n    write_packed(L, o.pk_lanes, r, k == 0 ? (uint32_t)L.frame_count : (over",
+     "outputs: EnvironmentState / obs / info (BC:449-468, FE:336-380)"),
 ]
 RARE_TAG = "[rare]"
 # functions charged wherever they sit in the chain (the rare work nested inside a common phase)

@@ -22,7 +22,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-LEGS = ["step", "step_warm_first", "host_actions", "step_gather", "venv_torch", "venv_numpy", "single_env"]
+# in marker order; the "warm_*" sections (warm-ups between the timed legs) are traced but not reported
+LEGS = ["step", "step_warm_first", "host_actions", "step_gather", "warm_venv_torch", "venv_torch", "warm_venv_numpy",
+        "venv_numpy", "warm_single_env", "single_env"]
 
 
 def run(n, steps):
@@ -90,6 +92,7 @@ def run(n, steps):
         env = FootsiesVectorEnv(n, opponent=lambda o, i: r2[k[0]], output=kind, seed=0,
                                 retain_host_heap=kind == "numpy")
         env.reset(seed=0)
+        marker()
         for j in range(400):
             k[0] = j
             env.step(acts[j])
@@ -103,6 +106,7 @@ def run(n, steps):
     env = FootsiesEnv(seed=0)
     env.reset(seed=0)
     acts = [tuple(bool(b) for b in row) for row in rng.integers(0, 2, (520, 3))]
+    marker()
     for j in range(20):
         if env.step(acts[j])[2]:
             env.reset()
@@ -139,6 +143,8 @@ def reduce(d, out_json):
     out = {"source": os.path.relpath(path, ROOT) if path.startswith(ROOT) else path,
            "command": "rocprofv3 --kernel-trace --output-format csv -- python3 tools/kstep_legs.py", "legs": {}}
     for leg, ds in legs.items():
+        if leg.startswith("warm_"):
+            continue
         dur = sorted(e - s for s, e, _ in ds)
         starts = [s for s, _, _ in ds]
         gaps = sorted(b - a for a, b in zip(starts, starts[1:]))
@@ -147,7 +153,7 @@ def reduce(d, out_json):
                             "median_us": q(dur, 0.5), "min_us": dur[0] / 1e3, "p99_us": q(dur, 0.99),
                             "max_us": dur[-1] / 1e3,
                             "period_median_us": q(gaps, 0.5) if gaps else None}
-    alld = [e - s for ds in legs.values() for s, e, _ in ds]
+    alld = [e - s for leg, ds in legs.items() if not leg.startswith("warm_") for s, e, _ in ds]
     out["all_legs_avg_us"] = sum(alld) / len(alld) / 1e3 if alld else None
     with open(out_json, "w") as f:
         json.dump(out, f, indent=1)
