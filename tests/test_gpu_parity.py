@@ -248,7 +248,12 @@ def test_standard_load_leaves_the_general_geometry_path():
     st["f"][5, 0]["position_y"] = np.float32(0.5)
     sim.set_state(st)
     assert name() == "fsk::k_step_n<0, 0>"
-    st["f"][5, 0]["position_y"] = np.float32(-0.0)  # -0.0 is ground level
+    # -0.0 is ground level for the boxes, but the pushes keep its sign and the round start writes
+    # +0.0 (SetupBattleStart, F:120-135): only the general-geometry tick carries y
+    st["f"][5, 0]["position_y"] = np.float32(-0.0)
+    sim.set_state(st)
+    assert name() == "fsk::k_step_n<0, 0>"
+    st["f"][5, 0]["position_y"] = np.float32(0.0)
     sim.set_state(st)
     assert name() == "fsk::k_step_n1<0, 0>"
     st["f"][7, 1]["facing_flipped"] = 1
