@@ -511,8 +511,83 @@ def kat_attack_table_rows(backend):
                 assert s[D_ + "Position"] == step_x(xd1, velocity(DAMAGE, 0), dsign), (label, guard)
 
 
+# ---------------------------------------------------------------------------------------------
+# UpdateActionRequest's request order and RequestAction's rules, from inputs
+# ---------------------------------------------------------------------------------------------
+def kat_request_chain(backend):
+    """UpdateActionRequest (F:201-286) requests, in order: the special or the attack, the dash,
+    then the movement; RequestAction (F:472-510) sets an action when the current one has ended
+    (isActionEnd: frame >= frameCount, F:90), never re-sets the current action, and otherwise only
+    from an always-cancelable action or through a cancel window.  Hand-derived from data/f00.json:
+    * Attack pressed with a direction held (forward, backward or both; P2's forward is Left) is
+      B_ATTACK, without one N_ATTACK (F:247-253); the movement request after it finds B_ATTACK at
+      frame 0 with no cancel window and does nothing, and B_ATTACK has no movement: x stays;
+    * FORWARD held for 50 ticks: the same-action request is refused, so the frame counts 0 .. 23;
+      on the tick it reaches frameCount 24 the action has ended and FORWARD is set again at 0
+      (frames 0..23, 0..23, 0, 1), walking every tick;
+    * N_ATTACK pressed again: on frame 21 (not ended) the press requests N_SPECIAL (F:243-246),
+      which no window of frame 21 takes -- nothing happens and STAND follows on frame 22; on the
+      tick its frame reaches 22 (ended) the press requests N_ATTACK, which is set at frame 0;
+    * a forward tap, a neutral frame, then forward + Attack: the dash input is there (taps two
+      frames apart), but B_ATTACK is requested first and the dash request that follows finds
+      B_ATTACK at frame 0 with no cancel window (F:256-259): B_ATTACK, no dash;
+    * B_ATTACK's execute window (frames 3-5, N_SPECIAL): Attack pressed on the tick B_ATTACK's real
+      hitbox lands (frame 3) buffers N_SPECIAL; the hit stuns both for 12 (ATK B_ATTACK); on the
+      tick the stun reaches 0 the buffer is taken (a landed hit: canCancelAttack, F:222-229):
+      N_SPECIAL frame 0, moving by its frame-0 velocity 2."""
+    fwd_speed = _fighter_data()["forward_move_speed"]
+    assert ACTIONS[FORWARD]["frame_count"] == 24 and ACTIONS[FORWARD]["always_cancelable"]
+    assert ACTIONS[N_ATTACK]["frame_count"] == 22 and not ACTIONS[B_ATTACK]["movements"]
+    assert ACTIONS[B_ATTACK]["cancels"] == [
+        {"win": [1, 2], "buffer": True, "execute": False, "action_ids": [N_SPECIAL]},
+        {"win": [3, 5], "buffer": False, "execute": True, "action_ids": [N_SPECIAL]}]
+    # Attack with / without a direction, both players
+    for who in (0, 1):
+        for d, act in ((0, N_ATTACK), (R, B_ATTACK), (L, B_ATTACK), (L | R, B_ATTACK)):
+            fresh(backend)
+            backend.step(_a(A | d if who == 0 else 0), _a(A | d if who == 1 else 0))
+            s = backend.env_state()[0]
+            key = "p1" if who == 0 else "p2"
+            assert (s[key + "Move"], s[key + "MoveFrame"]) == (act, 0), (who, d, s[key + "Move"])
+            assert s[key + "Position"] == (F32(-2) if who == 0 else F32(2)), (who, d)
+    # FORWARD held: the frame cycles through 0..23
+    fresh(backend)
+    st, _ = run(backend, lambda t: R, lambda t: 0, 50)
+    x = F32(-2)
+    for t in range(50):
+        x = step_x(x, fwd_speed, 1)
+        assert (st[t]["p1Move"], st[t]["p1MoveFrame"]) == (FORWARD, t % 24), (t, st[t]["p1MoveFrame"])
+        assert st[t]["p1Position"] == x, t
+    # N_ATTACK pressed again on frame 21 / on the tick it ends (frame 22)
+    for press, expect in ((21, (N_ATTACK, 21, STAND, 0)), (22, (N_ATTACK, 21, N_ATTACK, 0))):
+        fresh(backend)
+        st, _ = run(backend, lambda t, press=press: A if t in (0, press) else 0, lambda t: 0, 23)
+        assert (st[21]["p1Move"], st[21]["p1MoveFrame"], st[22]["p1Move"], st[22]["p1MoveFrame"]) == expect, press
+        assert all((st[t]["p1Move"], st[t]["p1MoveFrame"]) == (N_ATTACK, t) for t in range(21)), press
+    # the attack request comes before the dash request
+    fresh(backend)
+    st, _ = run(backend, lambda t: (R, 0, R | A)[t], lambda t: 0, 3)
+    assert [st[t]["p1Move"] for t in range(3)] == [FORWARD, STAND, B_ATTACK], [st[t]["p1Move"] for t in range(3)]
+    assert st[2]["p1MoveFrame"] == 0 and st[2]["p1Position"] == step_x(F32(-2), fwd_speed, 1)
+    # B_ATTACK -> N_SPECIAL through the execute window after a landed hit (P1 loaded at frame 2,
+    # P2 standing 2.0 away: the real hitbox [x1, x1 + 1.6] reaches P2's hurtbox [0.25, 1.75])
+    fresh(backend)
+    load(backend, (-1.0, B_ATTACK, 2), (1.0, STAND, 0))
+    st, _ = run(backend, lambda t: A if t == 0 else 0, lambda t: 0, 14)
+    h = st[0]
+    assert (h["p1Move"], h["p1MoveFrame"], h["p2Move"], h["p1Hitstun"], h["p2Hitstun"]) == (B_ATTACK, 3, DAMAGE, 12, 12)
+    assert int(backend.state()[0]["f"][0]["buffer_action_id"]) == -1  # (taken by tick 12, see below)
+    for t in range(1, 12):
+        assert (st[t]["p1Move"], st[t]["p1MoveFrame"], st[t]["p1Hitstun"]) == (B_ATTACK, 3, 12 - t), t
+    s = st[12]
+    assert (s["p1Move"], s["p1MoveFrame"], s["p1Hitstun"]) == (N_SPECIAL, 0, 0), s["p1Move"]
+    assert s["p1Position"] == step_x(F32(-1.0), velocity(N_SPECIAL, 0), 1)
+    assert (st[13]["p1Move"], st[13]["p1MoveFrame"]) == (N_SPECIAL, 1)
+
+
 ALL = {
     "attack_table_rows": kat_attack_table_rows,
+    "request_chain": kat_request_chain,
     "b_special_windows": kat_b_special_windows,
     "dash_edges": kat_dash_edges,
     "intro_stale_input": kat_intro_stale_input,
@@ -523,6 +598,8 @@ ALL = {
 
 # The C# paths each scenario pins (DESIGN.md section 3 reproduces this table)
 PINS = {
+    "request_chain": "F:201-286 request order (special / attack, dash, movement), F:472-510 ended / same-action / "
+                     "cancel-window rules, B_ATTACK's execute window taken at stun 0 after a hit (F:222-229)",
     "attack_table_rows": "F:357-398, 446-454 + ATK:14-54: every attack's guardAction / guardStun, damageAction / hitStun, "
                          "guardBreakStun with GUARD_BREAK reserved, as P1 and as P2 (BC:523-586)",
     "b_special_windows": "AD:150-161 first-match GetMovementData over ACT/B_SPECIAL.asset:14-83's overlapping windows",

@@ -49,7 +49,8 @@ def variant_source():
     b = "  if constexpr (FUSED) stage_tables<P2 == FS_P2_BOT || P2 == kActors>();\n"
     assert b in s
     s = s.replace(b, b + "  const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();\n", 1)
-    c = "  if (active) store_lane<P2>(L, p.st, a);\n}\n"
+    c = ("  if (active) {\n    store_lane<P2>(L, p.st, a);\n"
+         "    if constexpr (GEOM) reinterpret_cast<float*>(p.st.posy)[2 * a + (int)k] = L.f.y;\n  }\n}\n")
     assert c in s
     s = s.replace(c, (
         "  const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();\n"
@@ -74,7 +75,7 @@ def build():
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "build_variant.py"), src, OUT], check=True)
 
 
-def run(envs, reps):
+def run(envs, reps, packed=False):
     os.environ["FOOTSIES_LIB"] = os.path.join(OUT, "libfootsies.so")
     import torch
 
@@ -90,14 +91,22 @@ def run(envs, reps):
     h = sim.handle
     tmax = 1000
     p1, p2 = sim.hash_actions(tmax, seed=0x5EED, t0=0)
-    traj = sim.alloc_trajectory(tmax)
-    td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
+    if packed:  # the bench's layout (fs_step_n_packed)
+        traj = sim.alloc_packed_trajectory(tmax)
+        td = _abi.fs_packed_traj(lanes=traj["lanes"].data_ptr(), reward=traj["reward"].data_ptr(),
+                                 final_lanes=traj["final_lanes"].data_ptr())
+    else:
+        traj = sim.alloc_trajectory(tmax)
+        td = _abi.fs_outputs(**{k: traj[k].data_ptr() for k in _abi.OUTPUT_SPEC})
     b1, b2 = p1.data_ptr(), p2.data_ptr()
     waves = (2 * N + 63) // 64
     buf = (C.c_uint64 * (waves * NSTAMP))()
 
     def launch(n):
-        check(L.fs_step_n(h, n, C.c_void_p(b1), C.c_void_p(b2), 0, C.byref(td)), h)
+        if packed:
+            check(L.fs_step_n_packed(h, n, C.c_void_p(b1), C.c_void_p(b2), C.byref(td)), h)
+        else:
+            check(L.fs_step_n(h, n, C.c_void_p(b1), C.c_void_p(b2), 0, C.byref(td)), h)
 
     # warm the clock and the pages
     for _ in range(3):
@@ -138,6 +147,13 @@ def run(envs, reps):
         xcc = {}
         for s in st:
             xcc.setdefault(int(s[5]) & 0xF, []).append(us(s[0]))
+        # the waves sharing a SIMD (HW_ID: wave slot 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13 -- with the XCC):
+        # how far apart their loops end, and how long the last one runs alone
+        simd = {}
+        for s in st:
+            hw = int(s[4])
+            simd.setdefault((int(s[5]) & 0xF, (hw >> 13) & 7, (hw >> 8) & 31, (hw >> 4) & 3), []).append(s)
+        gaps = sorted((max(x[2] for x in g) - min(x[2] for x in g)) / 100.0 for g in simd.values() if len(g) > 1)
         res["shapes"].append({
             "ticks": n, "b2b_us": round(b2b, 2), "isolated_wall_us": round(statistics.median(walls), 2),
             "wave_start_us": {"p0": 0.0, "p50": round(q(starts, .5), 2), "p90": round(q(starts, .9), 2),
@@ -147,6 +163,8 @@ def run(envs, reps):
             "loop_us_per_tick_p50": round(q(loop, .5) / n, 4),
             "drain_us": {"p50": round(q(drain, .5), 2), "max": round(drain[-1], 2)},
             "wave_end_us": {"p50": round(q(ends, .5), 2), "max": round(ends[-1], 2)},
+            "simd_pair_loop_end_gap_us": {"p50": round(q(gaps, .5), 2), "p90": round(q(gaps, .9), 2),
+                                          "max": round(gaps[-1], 2)} if gaps else None,
             "first_start_by_xcc_us": {str(k): round(min(v), 2) for k, v in sorted(xcc.items())},
             "last_start_by_xcc_us": {str(k): round(max(v), 2) for k, v in sorted(xcc.items())},
         })
@@ -163,11 +181,12 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "timeline.json"))
+    ap.add_argument("--packed", action="store_true", help="fs_step_n_packed launches (the bench's layout)")
     a = ap.parse_args()
     if a.cmd == "build":
         build()
         return
-    res = run(a.envs, a.reps)
+    res = run(a.envs, a.reps, a.packed)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
