@@ -512,10 +512,15 @@ __device__ __forceinline__ void step_body1(const StepParams& p) {
                  : "v"(fl1[j]), "v"(fl2[j]) : "memory");
   }
   // one tick in slot J = t mod D (a compile-time index, so the slots stay in registers)
+  // time-sliced wave priority (prio_slice), as in the two-lane loop: from two waves per SIMD
+  // (131 072 arenas) it keeps a SIMD's waves progressing together (+4.9 % remote P2, +7.1 % bot
+  // at 131 072 arenas, profiles/r05g_ab_onelane_prio_131k.txt)
+  const uint32_t grp = prio_group();
   auto tick = [&](int t, auto J) {
     constexpr int j = decltype(J)::value, jn = (j + 1) % D;
     fl1[j] = issue1(t + D);
     fl2[j] = issue2(t + D);
+    if (p.prio) prio_slice(grp);
     uint32_t n1 = fl1[jn], n2 = fl2[jn];
     env_step1<FM, P2, W, PK>(A, rd1 & 7u, rd2 & 7u, p, (uint32_t)t * row_step + (uint32_t)a, n1, n2);
     rd1 = n1;

@@ -2169,17 +2169,19 @@ static bool fused_one_lane(int n_envs) {
   return n_envs >= threshold;
 }
 
-// Whether a two-lane fused launch over n_envs arenas holds more than one wave per SIMD, the case
-// prio_slice is for.  FOOTSIES_PRIO=0 / 1 forces it off / on (A/B timing).
-static bool two_waves_per_simd(int n_envs) {
+// Whether a fused launch with `lanes` lanes (two per arena, or one for the one-lane kernel) holds
+// more than one wave per SIMD, the case prio_slice is for.  FOOTSIES_PRIO=0 / 1 forces it off / on
+// (A/B timing).
+static bool waves_above_simds(int64_t lanes) {
   static const int forced = [] {
     const char* e = getenv("FOOTSIES_PRIO");
     return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' + 1 : 0;
   }();
   if (forced) return forced == 2;
   static const int simds = simd_count();
-  return (2 * (int64_t)n_envs + 63) / 64 > simds;
+  return (lanes + 63) / 64 > simds;
 }
+static bool two_waves_per_simd(int n_envs) { return waves_above_simds(2 * (int64_t)n_envs); }
 
 // Whether a two-lane fused row launch prepares each tick's request at the end of the tick before
 // (Pre / prepare_request): at one wave per SIMD, where no partner wave issues in that LDS wait
@@ -2205,6 +2207,7 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   else if (p.out.pk_lanes) {  // (rows: fs_api checks)
     if constexpr (P2 != kActors) {
       if (!p.geom && fused_one_lane(p.n_envs)) {
+        p.prio = waves_above_simds(p.n_envs);  // (one lane per arena)
         hipLaunchKernelGGL((k_step_n1_packed<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
         return;
       }
@@ -2215,8 +2218,12 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
   else if constexpr (P2 != kActors) {
     // (the one-lane kernel has no general-geometry tick: a geom launch takes the two-lane one)
-    if (!p.geom && fused_one_lane(p.n_envs)) hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
-    else hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
+    if (!p.geom && fused_one_lane(p.n_envs)) {
+      p.prio = waves_above_simds(p.n_envs);  // (one lane per arena)
+      hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
+    } else {
+      hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
+    }
   } else {
     hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
   }
