@@ -512,9 +512,8 @@ __device__ __forceinline__ void step_body1(const StepParams& p) {
                  : "v"(fl1[j]), "v"(fl2[j]) : "memory");
   }
   // one tick in slot J = t mod D (a compile-time index, so the slots stay in registers)
-  // time-sliced wave priority (prio_slice), as in the two-lane loop: from two waves per SIMD
-  // (131 072 arenas) it keeps a SIMD's waves progressing together (+4.9 % remote P2, +7.1 % bot
-  // at 131 072 arenas, profiles/r05g_ab_onelane_prio_131k.txt)
+  // time-sliced wave priority (prio_slice), as in the two-lane loop: at two waves per SIMD (131 072
+  // arenas) it keeps a SIMD's waves progressing together (fs_kernels.hip one_lane_prio)
   const uint32_t grp = prio_group();
   auto tick = [&](int t, auto J) {
     constexpr int j = decltype(J)::value, jn = (j + 1) % D;

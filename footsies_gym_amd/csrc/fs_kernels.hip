@@ -2172,16 +2172,28 @@ static bool fused_one_lane(int n_envs) {
 // Whether a fused launch with `lanes` lanes (two per arena, or one for the one-lane kernel) holds
 // more than one wave per SIMD, the case prio_slice is for.  FOOTSIES_PRIO=0 / 1 forces it off / on
 // (A/B timing).
-static bool waves_above_simds(int64_t lanes) {
+static int prio_forced() {  // 0: not forced, 1: off, 2: on
   static const int forced = [] {
     const char* e = getenv("FOOTSIES_PRIO");
     return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' + 1 : 0;
   }();
-  if (forced) return forced == 2;
+  return forced;
+}
+static bool waves_above_simds(int64_t lanes) {
+  if (prio_forced()) return prio_forced() == 2;
   static const int simds = simd_count();
   return (lanes + 63) / 64 > simds;
 }
 static bool two_waves_per_simd(int n_envs) { return waves_above_simds(2 * (int64_t)n_envs); }
+// The one-lane kernels: the slicing pays at two waves per SIMD (131 072 arenas: +4.4 % / +4.9 % remote
+// P2, +4.1 % / +7.1 % bot, per-field / packed) and costs the remote-P2 case at four (262 144: -2.3 %,
+// bot +3.3 %; profiles/r05g_ab_onelane_prio_131k.txt, r05h_ab_onelane_prio_*.txt), so only there.
+static bool one_lane_prio(int n_envs) {
+  if (prio_forced()) return prio_forced() == 2;
+  static const int simds = simd_count();
+  const int64_t waves = ((int64_t)n_envs + 63) / 64;
+  return waves > simds && waves <= 2 * (int64_t)simds;
+}
 
 // Whether a two-lane fused row launch prepares each tick's request at the end of the tick before
 // (Pre / prepare_request): at one wave per SIMD, where no partner wave issues in that LDS wait
@@ -2207,7 +2219,7 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   else if (p.out.pk_lanes) {  // (rows: fs_api checks)
     if constexpr (P2 != kActors) {
       if (!p.geom && fused_one_lane(p.n_envs)) {
-        p.prio = waves_above_simds(p.n_envs);  // (one lane per arena)
+        p.prio = one_lane_prio(p.n_envs);
         hipLaunchKernelGGL((k_step_n1_packed<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
         return;
       }
@@ -2219,7 +2231,7 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   else if constexpr (P2 != kActors) {
     // (the one-lane kernel has no general-geometry tick: a geom launch takes the two-lane one)
     if (!p.geom && fused_one_lane(p.n_envs)) {
-      p.prio = waves_above_simds(p.n_envs);  // (one lane per arena)
+      p.prio = one_lane_prio(p.n_envs);
       hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
     } else {
       hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);

@@ -493,6 +493,12 @@ def test_bench_json_contract(extra):
     assert d["scaling"] == ("strong" if extra else "weak")
     r = d["roofline"]
     assert r["bound"] in ("hbm", "simd-issue") and 0 < r["frac"] < 1 and r["achieved"] == pytest.approx(r["frac"] * r["peak"])
+    # the byte accounting: algorithmic (2 B in + 38 B out per env-step, 96 B of state per arena and
+    # launch) and the packed layout's 2 B in + 40 B out beside it
+    n, t = d["config"]["envs_per_gpu"], r["ticks_per_launch"]
+    assert r["algorithmic_bytes_per_launch"] == n * (96 + 40 * t)
+    assert r["layout_bytes_per_launch"] == n * (96 + 42 * t)
+    assert r["traffic_ratio"] is None or r["traffic_ratio"] == pytest.approx(r["traffic"] / r["algorithmic_bytes_per_launch"])
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] >= 1
 
 
