@@ -21,9 +21,9 @@ One iteration:
    recomputed in fp32 (`old_logp="fp32"`, first ratio exactly 1).  Either way the iteration
    reports how far the two are apart: `kl_behaviour_fp32`, the sample estimate
    E_a~behaviour[log p_bf16(a) - log p_fp32(a)] of KL(bf16 actor || fp32 actor), and
-   `logp_abs_diff`, the mean |log p_bf16(a) - log p_fp32(a)|.  The fp32 log-probs and the
-   critic values come from fs_ppo_eval at fp32 FMAs (FS_PPO_FP32) whatever the learner's
-   precision; only the gradients use `learner_precision`.
+   `logp_abs_diff`, the mean |log p_bf16(a) - log p_fp32(a)|.  The fp32 log-probs come from
+   fs_ppo_eval at fp32 FMAs (FS_PPO_FP32) whatever the learner's precision; the critic values and
+   the gradients use `learner_precision`.
 4. The new actor weights are copied into the rollout's device buffers (no reallocation).
 
 Nothing leaves the GPU inside an iteration, and the simulator never waits on the host.
@@ -389,10 +389,15 @@ class PPOTrainer:
             x = feats[:T].reshape(M, N_FEATURES)
             a = actions.reshape(M)
             behav = self.logp.reshape(M)  # what the kernel sampled with (bf16 actor)
-            if self._grad is not None:  # both forward passes, GAE and the sample table: five launches
-                # always at fp32 FMAs, whatever the learner's precision: old32 is the fp32 reference
-                # the KL diagnostic and old_logp="fp32" are defined against
-                v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk, precision="fp32")
+            if self._grad is not None:  # the forward passes, GAE and the sample table
+                # old32 -- the fp32 reference the KL diagnostic and old_logp="fp32" are defined
+                # against -- always at fp32 FMAs, whatever the learner's precision; the critic values
+                # (GAE's baseline) at the learner's own precision
+                if nk == M:
+                    v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk, precision="fp32")
+                else:
+                    v, _ = self._grad.evaluate(feats.view(-1, N_FEATURES))
+                    _, old32 = self._grad.evaluate(x[:nk].contiguous(), a, nk, precision="fp32")
                 values = v.view(T + 1, N)
                 adv, ret = gae_device(rewards, dones, values, self.gamma, self.lam)
                 old = behav if self.old_logp == "behaviour" else old32
