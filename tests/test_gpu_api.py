@@ -497,7 +497,8 @@ def test_bench_json_contract(extra):
     # launch) and the packed layout's 2 B in + 40 B out beside it
     n, t = d["config"]["envs_per_gpu"], r["ticks_per_launch"]
     assert r["algorithmic_bytes_per_launch"] == n * (96 + 40 * t)
-    assert r["layout_bytes_per_launch"] == n * (96 + 42 * t)
+    packed = d["config"]["mode"] == "fused" and d["config"]["trajectory"].startswith("packed")
+    assert r["layout_bytes_per_launch"] == n * (96 + (42 if packed else 40) * t)
     assert r["traffic_ratio"] is None or r["traffic_ratio"] == pytest.approx(r["traffic"] / r["algorithmic_bytes_per_launch"])
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] >= 1
 
