@@ -117,7 +117,7 @@ def occupancy_plateau(path, packed=False):
     out = {}
     if not path or not os.path.exists(path):
         return out
-    pat = (r"packed\s+[\d.]+ us \(([\d.e+]+)\)" if packed else
+    pat = (r"packed\s+[\d.]+ us \(([\d.e+]+)[,)]" if packed else
            r"FUSED_LANES=2\s+C3\s+[\d.]+ us \(([\d.e+]+) env-steps/s")
     for line in open(path):
         m = re.search(pat, line)
