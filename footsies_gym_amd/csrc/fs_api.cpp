@@ -819,7 +819,8 @@ FS_API int fs_set_stream(fs_handle h, void* stream) {
 FS_API const char* fs_step_kernel(fs_handle h, int n_steps, int flags) {
   if (!h || n_steps <= 0 || (flags & ~(FS_KERNEL_HASHED | FS_KERNEL_POLICY | FS_KERNEL_PACKED))) return nullptr;
   return fsk::step_kernel_name((flags & FS_KERNEL_POLICY) != 0, (flags & FS_KERNEL_HASHED) != 0, n_steps, h->n,
-                               h->cfg.float_mode, variant(h), h->geom, (flags & FS_KERNEL_PACKED) != 0);
+                               h->cfg.float_mode, variant(h), h->geom, (flags & FS_KERNEL_PACKED) != 0,
+                               h->cfg.autoreset_mode);
 }
 
 FS_API int fs_num_envs(fs_handle h) { return h ? h->n : 0; }

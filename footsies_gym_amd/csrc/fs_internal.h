@@ -134,7 +134,7 @@ struct DelayParams {
 // variant: FS_P2_EXTERNAL / FS_P2_BOT / FS_P2_NOOP or kActors (see above)
 hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStream_t s);
 const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant,
-                             bool geom, bool packed);
+                             bool geom, bool packed, int autoreset_mode);
 hipError_t launch_reset(const ResetParams& p, int float_mode, hipStream_t s);
 hipError_t launch_set_p2(const DevState& st, int bot, const uint8_t* mask, int n, hipStream_t s);
 hipError_t launch_hash_actions(int n_envs, int n_steps, uint64_t seed, uint64_t t0, uint64_t arena_base, uint8_t* p1,

@@ -1843,33 +1843,28 @@ __global__ __launch_bounds__(256) void k_step(StepParams p) {
 // uniform over the launch) as two loops: the standard loop carries none of the y state.
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n(StepParams p) {
-  if (p.geom) {
-    step_body<FM, P2, true, false, false, true>(p);
-    return;
-  }
-  if constexpr (P2 != kActors) {
-    if (p.prefetch) {
-      step_body<FM, P2, true, false, false, false, false, true>(p);
-      return;
-    }
-  }
-  step_body<FM, P2, true, false>(p);
+  if (p.geom) step_body<FM, P2, true, false, false, true>(p);
+  else step_body<FM, P2, true, false>(p);
 }
 
 // fs_step_n_packed: the row loop of k_step_n storing packed trajectory records
 template <int FM, int P2>
 __global__ __launch_bounds__(256) void k_step_n_packed(StepParams p) {
-  if (p.geom) {
-    step_body<FM, P2, true, false, false, true, true>(p);
-    return;
-  }
-  if constexpr (P2 != kActors) {
-    if (p.prefetch) {
-      step_body<FM, P2, true, false, false, false, true, true>(p);
-      return;
-    }
-  }
-  step_body<FM, P2, true, false, false, false, true>(p);
+  if (p.geom) step_body<FM, P2, true, false, false, true, true>(p);
+  else step_body<FM, P2, true, false, false, false, true>(p);
+}
+
+// The same row loops with each tick's request prepared at the end of the tick before
+// (StepParams::prefetch; one wave per SIMD).  Kernels of their own: the prepared request stays live
+// across the loop's back edge, and in a shared kernel its registers would lower the standard loop's
+// occupancy too (132 VGPRs instead of 122: three waves per SIMD instead of four).
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step_n_pf(StepParams p) {
+  step_body<FM, P2, true, false, false, false, false, true>(p);
+}
+template <int FM, int P2>
+__global__ __launch_bounds__(256) void k_step_n_packed_pf(StepParams p) {
+  step_body<FM, P2, true, false, false, false, true, true>(p);
 }
 
 template <int FM, int P2>
@@ -2224,6 +2219,12 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
         return;
       }
     }
+    if constexpr (P2 != kActors) {
+      if (p.prefetch) {
+        hipLaunchKernelGGL((k_step_n_packed_pf<FM, P2>), grid, block, 0, s, p);
+        return;
+      }
+    }
     hipLaunchKernelGGL((k_step_n_packed<FM, P2>), grid, block, 0, s, p);
   }
   else if (!p.p1) hipLaunchKernelGGL((k_step_n_hashed<FM, P2>), grid, block, 0, s, p);
@@ -2233,6 +2234,8 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
     if (!p.geom && fused_one_lane(p.n_envs)) {
       p.prio = one_lane_prio(p.n_envs);
       hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
+    } else if (p.prefetch) {
+      hipLaunchKernelGGL((k_step_n_pf<FM, P2>), grid, block, 0, s, p);
     } else {
       hipLaunchKernelGGL((k_step_n<FM, P2>), grid, block, 0, s, p);
     }
@@ -2259,11 +2262,18 @@ hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStre
 
 // The kernel launch_step_p2 runs for a launch of this shape, as rocprofv3 names it (fs_step_kernel).
 const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant, bool geom,
-                             bool packed) {
+                             bool packed, int autoreset_mode) {
   static thread_local char buf[64];
   const bool one = !policy && !hashed && variant != kActors && !geom && fused_one_lane(n_envs);
-  const char* k = policy ? "k_step_n_policy" : packed ? (one ? "k_step_n1_packed" : "k_step_n_packed")
-                : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step" : one ? "k_step_n1" : "k_step_n";
+  StepParams q{};  // the prefetch test of launch_step_p2 for a row launch of this shape
+  q.autoreset_mode = autoreset_mode;
+  q.geom = geom;
+  q.n_steps = n_steps;
+  q.n_envs = n_envs;
+  q.p1 = reinterpret_cast<const uint8_t*>(1);
+  const bool pf = !policy && !hashed && !one && variant != kActors && request_prefetch(q);
+  const char* k = policy ? "k_step_n_policy" : packed ? (one ? "k_step_n1_packed" : pf ? "k_step_n_packed_pf" : "k_step_n_packed")
+                : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step" : one ? "k_step_n1" : pf ? "k_step_n_pf" : "k_step_n";
   snprintf(buf, sizeof buf, "fsk::%s<%d, %d>", k, float_mode == FS_FLOAT_DOUBLE ? 1 : 0, variant);
   return buf;
 }

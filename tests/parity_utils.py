@@ -121,3 +121,15 @@ def random_states(n, rng, p2="external", p2_bot_frac=0.0, geom_frac=0.0):
         st[pre + "prev_distance"][idle] = 0.0
         st[pre + "prev_opponent_action"][idle] = 0
     return st
+
+
+def fused_kernel(name, n_envs, same_step=True, mi355x_simds=1024):
+    """The name fs_step_kernel gives a two-lane fused row launch (`name`, e.g. "fsk::k_step_n<0, 0>")
+    over n_envs arenas: the request-prefetch kernel (`..._pf`) at one wave per SIMD or less with
+    same-step auto-reset (fs_kernels.hip request_prefetch; FOOTSIES_PREFETCH=0 / 1 forces it)."""
+    import os
+    forced = os.environ.get("FOOTSIES_PREFETCH", "")
+    on = forced == "1" or (forced != "0" and (2 * n_envs + 63) // 64 <= mi355x_simds)
+    if not same_step or "<" not in name or ", 3>" in name:  # (next-step auto-reset, per-arena actors: never)
+        return name
+    return name.replace("<", "_pf<", 1) if on else name

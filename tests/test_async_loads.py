@@ -14,8 +14,9 @@ def test_no_register_touched_while_its_row_is_in_flight():
                        text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     # k_step_n (8 instances: 2 float modes x 4 P2 variants) and k_step_n_packed (8) read rows, and
-    # k_step_n1 and k_step_n1_packed (6 each: no kActors variant)
-    assert " 0 findings" in r.stdout and "28 kernels" in r.stdout, r.stdout
+    # k_step_n1 and k_step_n1_packed (6 each: no kActors variant), k_step_n_pf and k_step_n_packed_pf
+    # (6 each: the request prefetch never runs per-arena actors)
+    assert " 0 findings" in r.stdout and "40 kernels" in r.stdout, r.stdout
 
 
 def test_wait_counts_are_proven_and_a_too_deep_wait_is_caught(tmp_path):

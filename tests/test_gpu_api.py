@@ -10,7 +10,7 @@ from tests import kat_scenarios as kat
 from tests import wire_client, wire_replay
 from tests import wrapper_replay as wr
 from tests.gpu_backend import SimBackend, make
-from tests.parity_utils import compare_outputs, compare_states
+from tests.parity_utils import compare_outputs, compare_states, fused_kernel
 
 P2_MODES = {"external": _abi.FS_P2_EXTERNAL, "bot": _abi.FS_P2_BOT, "noop": _abi.FS_P2_NOOP}
 
@@ -517,13 +517,15 @@ def test_bench_extras_legs():
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, check=True).stdout
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     # (the side legs use the headline's trajectory layout, packed by default)
-    assert d["p2_bot_mode"]["kernel"] == "fsk::k_step_n_packed<0, 1>" and d["p2_bot_mode"]["value"] > 0
+    assert d["p2_bot_mode"]["kernel"] == fused_kernel("fsk::k_step_n_packed<0, 1>", 2048) and d["p2_bot_mode"]["value"] > 0
     for leg in ("mixed_p2", "by_example"):
         assert d["actors_mode"][leg]["kernel"] == "fsk::k_step_n_packed<0, 3>", d["actors_mode"]
         assert d["actors_mode"][leg]["value"] > 0
     # the headline's fused trajectory is packed by default; the per-field layout is timed beside
-    assert d["roofline"]["kernel"] == "fsk::k_step_n_packed<0, 0>" and d["config"]["trajectory"].startswith("packed")
-    assert d["fused_other_layout"]["kernel"] == "fsk::k_step_n<0, 0>" and d["fused_other_layout"]["value"] > 0
+    assert d["roofline"]["kernel"] == fused_kernel("fsk::k_step_n_packed<0, 0>", 2048)
+    assert d["config"]["trajectory"].startswith("packed")
+    assert d["fused_other_layout"]["kernel"] == fused_kernel("fsk::k_step_n<0, 0>", 2048)
+    assert d["fused_other_layout"]["value"] > 0
     v = d["vector_env"]["numpy"]
     assert v["steps"] >= 200 and v["warmup_steps"] >= 200 and v["terminals_per_step"] > 0
 
@@ -707,7 +709,7 @@ def test_step_kernel_names_the_launched_kernel():
     name = lambda s, n, fl=0: L.fs_step_kernel(s.handle, n, fl).decode()  # noqa: E731
     assert name(a, 1) == "fsk::k_step<0, 0>"
     forced = os.environ.get("FOOTSIES_FUSED_LANES", "")
-    assert name(a, 1000) == ("fsk::k_step_n1<0, 0>" if forced == "1" else "fsk::k_step_n<0, 0>")
+    assert name(a, 1000) == ("fsk::k_step_n1<0, 0>" if forced == "1" else fused_kernel("fsk::k_step_n<0, 0>", 64))
     assert name(a, 1000, 1) == "fsk::k_step_n_hashed<0, 0>" and name(a, 20, 2) == "fsk::k_step_n_policy<0, 0>"
     a.set_p2_mode("bot", np.arange(64) % 2 == 0)
     assert name(a, 1000) == "fsk::k_step_n<0, 3>"  # per-arena actors

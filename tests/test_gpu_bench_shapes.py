@@ -23,7 +23,7 @@ import numpy as np
 import pytest
 
 from footsies_gym_amd import _abi
-from tests.parity_utils import compare_outputs, compare_states
+from tests.parity_utils import compare_outputs, compare_states, fused_kernel
 
 pytestmark = pytest.mark.gpu
 
@@ -62,6 +62,8 @@ def test_c4_per_gpu_shape_matches_oracle(oracle_lib, actors, shape):
     """C4's per-GPU shape (262 144 arenas over 8 GPUs: 32 768 per GPU, one wave per SIMD), where
     the two-lane fused launches prepare each tick's request at the end of the tick before
     (StepParams::prefetch): the same bench shapes against the oracle."""
+    if os.environ.get("FOOTSIES_PREFETCH") != "0":
+        assert fused_kernel(KERNEL[actors], 32768).startswith("fsk::k_step_n_packed_pf<")
     run_shape(oracle_lib, actors, shape, 32768)
 
 
@@ -100,7 +102,8 @@ def run_shape(oracle_lib, actors, shape, n):
     h2 = p2.cpu().numpy() if ext else None
     biggest = max(launches)
     kname = lib().fs_step_kernel(sim.handle, biggest, _abi.FS_KERNEL_PACKED).decode()
-    assert kname == KERNEL[actors] or os.environ.get("FOOTSIES_FUSED_LANES") == "1", kname
+    want = fused_kernel(KERNEL[actors], n)
+    assert kname == want or os.environ.get("FOOTSIES_FUSED_LANES") == "1", kname
     traj = sim.alloc_packed_trajectory(biggest)
     k, checked = 0, 0
     for j, m in enumerate(launches):

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from footsies_gym_amd import _abi
-from tests.parity_utils import compare_states, random_states
+from tests.parity_utils import compare_states, fused_kernel, random_states
 
 pytestmark = pytest.mark.gpu
 
@@ -118,7 +118,7 @@ def test_packed_trajectory_argument_errors():
     from footsies_gym_amd._lib import lib  # the kernel a packed call runs, as rocprofv3 names it
     one = os.environ.get("FOOTSIES_FUSED_LANES") == "1"  # (test_gpu_one_lane.py's child forces the one-lane kernel)
     assert lib().fs_step_kernel(sim.handle, 4, _abi.FS_KERNEL_PACKED).decode() == (
-        "fsk::k_step_n1_packed<0, 0>" if one else "fsk::k_step_n_packed<0, 0>")
+        "fsk::k_step_n1_packed<0, 0>" if one else fused_kernel("fsk::k_step_n_packed<0, 0>", 64))
     torch.cuda.synchronize()
 
 
