@@ -2145,8 +2145,12 @@ static inline dim3 grid_for(int n) { return dim3((unsigned)((n + kBlock - 1) / k
 // per SIMD (65 536 arenas, C3) it exposes the tick's dependent LDS reads and runs 16-18 % slower;
 // from two waves per SIMD (131 072 arenas) on it matches the two-lane kernel with a remote P2 and
 // beats it by 12-25 % with the scripted bot.  So the one-lane kernel takes the
-// launches with at least two of its waves per SIMD.  FOOTSIES_FUSED_LANES=1 / 2 forces one kernel
-// (A/B timing, and the parity suite runs both).
+// launches with at least two of its waves per SIMD -- except packed launches with a remote P2 from
+// four of them on (262 144 arenas), where the two-lane packed kernel at 4 resident waves per SIMD is
+// ahead (+4.3 % at 262 144, +1.4 % at 524 288; 131 072: one lane +2.1 %; profiles/r05l_ab_lanes_*.txt,
+// r05m_ab_lanes_524288.txt); the per-field two-lane kernel, with its eight stores per tick, is not
+// (7.2e10 vs 7.8-7.9e10 at 262 144).
+// FOOTSIES_FUSED_LANES=1 / 2 forces one kernel (A/B timing, and the parity suite runs both).
 static int simd_count() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -2154,13 +2158,14 @@ static int simd_count() {
     cus = 256;  // MI355X
   return 4 * cus;
 }
-static bool fused_one_lane(int n_envs) {
+static bool fused_one_lane(int n_envs, int variant, bool packed) {
   static const int forced = [] {
     const char* e = getenv("FOOTSIES_FUSED_LANES");
     return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
   }();
   if (forced) return forced == 1;
-  static const int threshold = 2 * 64 * simd_count();
+  static const int64_t threshold = 2 * 64 * (int64_t)simd_count();
+  if (packed && variant == FS_P2_EXTERNAL) return n_envs >= threshold && n_envs < 2 * threshold;
   return n_envs >= threshold;
 }
 
@@ -2213,7 +2218,7 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
   else if (p.out.pk_lanes) {  // (rows: fs_api checks)
     if constexpr (P2 != kActors) {
-      if (!p.geom && fused_one_lane(p.n_envs)) {
+      if (!p.geom && fused_one_lane(p.n_envs, P2, true)) {
         p.prio = one_lane_prio(p.n_envs);
         hipLaunchKernelGGL((k_step_n1_packed<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
         return;
@@ -2231,7 +2236,7 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   else if (p.n_steps == 1) hipLaunchKernelGGL((k_step<FM, P2>), grid, block, 0, s, p);
   else if constexpr (P2 != kActors) {
     // (the one-lane kernel has no general-geometry tick: a geom launch takes the two-lane one)
-    if (!p.geom && fused_one_lane(p.n_envs)) {
+    if (!p.geom && fused_one_lane(p.n_envs, P2, false)) {
       p.prio = one_lane_prio(p.n_envs);
       hipLaunchKernelGGL((k_step_n1<FM, P2>), grid_for(p.n_envs), block, 0, s, p);
     } else if (p.prefetch) {
@@ -2264,7 +2269,7 @@ hipError_t launch_step(const StepParams& p, int float_mode, int variant, hipStre
 const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, int float_mode, int variant, bool geom,
                              bool packed, int autoreset_mode) {
   static thread_local char buf[64];
-  const bool one = !policy && !hashed && variant != kActors && !geom && fused_one_lane(n_envs);
+  const bool one = !policy && !hashed && variant != kActors && !geom && fused_one_lane(n_envs, variant, packed);
   StepParams q{};  // the prefetch test of launch_step_p2 for a row launch of this shape
   q.autoreset_mode = autoreset_mode;
   q.geom = geom;

@@ -722,3 +722,11 @@ def test_step_kernel_names_the_launched_kernel():
     if not forced:
         assert name(big, 1000) == "fsk::k_step_n1<0, 0>"  # two one-lane waves per SIMD on MI355X
     big.close()
+    # packed launches with a remote P2 from four one-lane waves per SIMD on: the two-lane kernel
+    # (fs_kernels.hip fused_one_lane); the scripted bot, and every per-field launch, keep the one-lane one
+    for p2, want in (("external", "fsk::k_step_n_packed<0, 0>"), ("bot", "fsk::k_step_n1_packed<0, 1>")):
+        huge = FootsiesSim(262144, p2_mode=p2)
+        if not forced:
+            assert name(huge, 1000, 4) == want, p2
+            assert name(huge, 1000) == "fsk::k_step_n1<0, %d>" % (p2 == "bot"), p2
+        huge.close()

@@ -85,14 +85,31 @@ def packed_vs_oracle(oracle_lib, N, launches, p2, seed=5):
 
 @pytest.mark.parametrize("N", [131072, 262144])
 @pytest.mark.parametrize("p2", ["external", "bot"])
-def test_one_lane_packed_kernel_at_its_sizes(oracle_lib, N, p2):
+def test_packed_kernel_at_c4_strong_scaling_sizes(oracle_lib, N, p2):
     """fs_step_n_packed at C4's one- and two-GPU strong-scaling shapes (262 144 and 131 072 arenas
-    per GPU) runs the one-lane packed kernel (k_step_n1_packed); its records against the oracle,
-    an even launch then an odd one (the row pipeline's tail)."""
-    if os.environ.get("FOOTSIES_FUSED_LANES") == "2":
-        pytest.skip("the two-lane kernel is forced")
+    per GPU): the one-lane packed kernel (k_step_n1_packed), except a remote P2's at 262 144, which
+    runs the two-lane one (fs_kernels.hip fused_one_lane); its records against the oracle, an even
+    launch then an odd one (the row pipeline's tail).  The forced runs (FOOTSIES_FUSED_LANES=1 / 2)
+    hold the other kernel at the same sizes."""
+    forced = os.environ.get("FOOTSIES_FUSED_LANES", "")
     name = packed_vs_oracle(oracle_lib, N, [24, 17], p2)
-    assert name == "fsk::k_step_n1_packed<0, %d>" % P2[p2], name
+    one = forced == "1" or (not forced and not (N == 262144 and p2 == "external"))
+    assert name == ("fsk::k_step_n1_packed<0, %d>" if one else "fsk::k_step_n_packed<0, %d>") % P2[p2], name
+
+
+def test_c4_sizes_with_each_kernel_forced():
+    """test_packed_kernel_at_c4_strong_scaling_sizes in child processes with the one-lane and the
+    two-lane kernel forced: both kernels against the oracle at 131 072 and 262 144 arenas, remote P2
+    and bot."""
+    if os.environ.get("FOOTSIES_FUSED_LANES"):
+        pytest.skip("already the child")
+    for lanes in ("1", "2"):
+        env = dict(os.environ, FOOTSIES_FUSED_LANES=lanes)
+        r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                            os.path.join(ROOT, "tests", "test_gpu_one_lane.py") + "::test_packed_kernel_at_c4_strong_scaling_sizes"],
+                           cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, lanes + r.stdout[-4000:] + r.stderr[-2000:]
+        assert "4 passed" in r.stdout, r.stdout[-2000:]
 
 
 @pytest.mark.parametrize("p2", ["external", "bot", "noop"])
