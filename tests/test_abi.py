@@ -106,3 +106,19 @@ def test_step_kernel_name_needs_a_handle(lib):
     f = lib.fs_step_kernel
     f.restype, f.argtypes = _abi.LIB_FUNCTIONS["fs_step_kernel"]
     assert f(None, 1, 0) is None
+
+
+def test_one_hip_runtime_per_process():
+    """The binding loads torch before libfootsies.so, so the library's libamdhip64.so.7 entry binds
+    to torch's runtime: one HIP and one HSA runtime per process.  Loaded the other way round the
+    process maps /opt/rocm's runtimes beside torch's, and fs_create found no device on the MI355X
+    box (profiles/r05q_*.log)."""
+    import subprocess
+    import sys
+    code = ("from footsies_gym_amd._lib import lib; lib(); import torch; "
+            "m = {l.split()[-1] for l in open('/proc/self/maps') if 'amdhip64' in l or 'hsa-runtime64' in l}; "
+            "print(sum('amdhip64' in x for x in m), sum('hsa-runtime64' in x for x in m))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[-2:] == ["1", "1"], r.stdout

@@ -5,8 +5,9 @@
 
 Each library is timed in its own subprocess (FOOTSIES_LIB override), rounds interleaved so
 box-level drift hits every variant alike.  Per library and P2 mode (external = C3, bot = C2):
-the median duration of back-to-back fs_step_n launches (fs_step_n_packed with --packed) of T
-ticks over N arenas with full trajectories, bracketed by HIP events on the launch stream.
+the median duration of back-to-back fs_step_n launches (fs_step_n_packed with --packed, or per
+library with @AB_PACKED=1 / 0) of T ticks over N arenas with full trajectories, bracketed by HIP
+events on the launch stream.
 """
 import argparse
 import os
@@ -16,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CODE = r'''
-import ctypes as C, sys, torch
+import ctypes as C, os, sys, torch
 sys.path.insert(0, %(root)r)
 from footsies_gym_amd import _abi
 from footsies_gym_amd._lib import check, lib
@@ -27,7 +28,7 @@ for mode in ("external", "bot"):
     sim = FootsiesSim(N, p2_mode=mode, seed=0)
     p1, p2 = sim.hash_actions(T, seed=0x5EED, p2=(mode == "external"))
     q2 = C.c_void_p(p2.data_ptr()) if mode == "external" else None
-    if %(packed)d:  # fs_step_n_packed into packed records (the bench's layout)
+    if int(os.environ.get("AB_PACKED", %(packed)d)):  # fs_step_n_packed into packed records (the bench's layout)
         traj = sim.alloc_packed_trajectory(T)
         td = _abi.fs_packed_traj(lanes=traj["lanes"].data_ptr(), reward=traj["reward"].data_ptr(),
                                  final_lanes=traj["final_lanes"].data_ptr())
