@@ -38,7 +38,7 @@ def lib():
         # torch first: its HIP runtime (libamdhip64.so.7, bundled with the wheel) is then the one the
         # library's DT_NEEDED entry binds to, so the process holds a single HIP / HSA runtime.  Loaded
         # the other way round, /opt/rocm's runtime comes in first and fs_create's hipGetDeviceCount
-        # failed on the MI355X box ("no ROCm-capable device", profiles/r05p_*.log).
+        # failed on the MI355X box ("no ROCm-capable device", profiles/r05q_lib_before_torch.log).
         import torch  # noqa: F401
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _abi.LIB_FUNCTIONS.items():

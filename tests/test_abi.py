@@ -112,7 +112,7 @@ def test_one_hip_runtime_per_process():
     """The binding loads torch before libfootsies.so, so the library's libamdhip64.so.7 entry binds
     to torch's runtime: one HIP and one HSA runtime per process.  Loaded the other way round the
     process maps /opt/rocm's runtimes beside torch's, and fs_create found no device on the MI355X
-    box (profiles/r05q_*.log)."""
+    box (profiles/r05q_lib_before_torch.log, r05p_lib_before_torch_test.log)."""
     import subprocess
     import sys
     code = ("from footsies_gym_amd._lib import lib; lib(); import torch; "
