@@ -77,11 +77,20 @@ typedef __bf16 BF8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ F16 mfma_bf16(BF8 a, BF8 b, F16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+// (as pairs: one v_cvt_pk_bf16_f32 rounds two values, one v_pk_add_f32 forms two remainders; the
+// library is built without SLP vectorization, so the pairs are spelled out)
+typedef float F2 __attribute__((ext_vector_type(2)));
+typedef __bf16 BF2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split8(const float (&x)[8], BF8& hi, BF8& lo) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    hi[j] = (__bf16)x[j];
-    lo[j] = (__bf16)(x[j] - (float)hi[j]);
+  for (int j = 0; j < 8; j += 2) {
+    const F2 v = {x[j], x[j + 1]};
+    const BF2 h = __builtin_convertvector(v, BF2);
+    const BF2 l = __builtin_convertvector(v - __builtin_convertvector(h, F2), BF2);
+    hi[j] = h[0];
+    hi[j + 1] = h[1];
+    lo[j] = l[0];
+    lo[j + 1] = l[1];
   }
 }
 // the three products of one K = 16 step, the small ones first
@@ -113,8 +122,28 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return copysignf(ax < 0.625f ? small : big, x);
 }
 
+// The split-bf16 precision's transcendentals: the hardware exp2 and reciprocal alone, without
+// tanh_fast's small-|x| polynomial and select or expf's range reduction.  tanh as
+// 1 - 2 / (2^(2 x log2 e) + 1) is within 2.5e-7 of tanh absolutely (the cancellation near 0 costs
+// relative accuracy, not absolute: far below the bf16 split's 2^-17 per product), exp within a
+// few ulp.  The fp32 precision keeps tanh_fast / expf.
+__device__ __forceinline__ float tanh_hw(float x) {
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(x * 2.8853900817779268f) + 1.f), 1.f);
+}
+template <bool HW>
+__device__ __forceinline__ float tanh_of(float x) {
+  if constexpr (HW) return tanh_hw(x);
+  else return tanh_fast(x);
+}
+template <bool HW>
+__device__ __forceinline__ float exp_of(float x) {
+  if constexpr (HW) return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+  else return expf(x);
+}
+
 // PPO's actor loss of one sample (ppo.py update) from its logits z: log_softmax, the clipped
 // surrogate and the entropy bonus; g3 = d loss / d z (zero for padding rows, !valid).
+template <bool HW>
 __device__ __forceinline__ void actor_loss(const float (&z)[8], const float (&tail)[4], bool valid, const Coef& c,
                                            float (&g3)[8], float& pg_sum, float& ent_sum) {
   float m = z[0];
@@ -122,7 +151,7 @@ __device__ __forceinline__ void actor_loss(const float (&z)[8], const float (&ta
   for (int o = 1; o < 8; ++o) m = fmaxf(m, z[o]);
   float se = 0.f;
 #pragma unroll
-  for (int o = 0; o < 8; ++o) se += expf(z[o] - m);
+  for (int o = 0; o < 8; ++o) se += exp_of<HW>(z[o] - m);
   const float lse = m + logf(se);
   float lp[8], p[8];
   const int act = (int)tail[0];
@@ -130,12 +159,12 @@ __device__ __forceinline__ void actor_loss(const float (&z)[8], const float (&ta
 #pragma unroll
   for (int o = 0; o < 8; ++o) {
     lp[o] = z[o] - lse;
-    p[o] = expf(lp[o]);
+    p[o] = exp_of<HW>(lp[o]);
     lp_a = o == act ? lp[o] : lp_a;
     ent -= p[o] * lp[o];
   }
   const float adv = tail[2];
-  const float rt = expf(lp_a - tail[1]);
+  const float rt = exp_of<HW>(lp_a - tail[1]);
   const float s1 = rt * adv, rc = fminf(fmaxf(rt, 1.f - c.clip), 1.f + c.clip), s2 = rc * adv;
   // torch.min's gradient goes to the smaller operand (half to each on a tie); clamp's passes
   // inside [1 - clip, 1 + clip]
@@ -172,11 +201,12 @@ __device__ __forceinline__ void store_rows(float* dst, const F16& v, int hf) {
   for (int qq = 0; qq < 4; ++qq)
     *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) = make_float4(v[4 * qq], v[4 * qq + 1], v[4 * qq + 2], v[4 * qq + 3]);
 }
+template <bool HW>
 __device__ __forceinline__ void store_rows_tanh(float* dst, const F16& v, int hf) {
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq)
-    *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) =
-        make_float4(tanh_fast(v[4 * qq]), tanh_fast(v[4 * qq + 1]), tanh_fast(v[4 * qq + 2]), tanh_fast(v[4 * qq + 3]));
+    *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) = make_float4(tanh_of<HW>(v[4 * qq]), tanh_of<HW>(v[4 * qq + 1]),
+                                                                    tanh_of<HW>(v[4 * qq + 2]), tanh_of<HW>(v[4 * qq + 3]));
 }
 
 #ifndef FSL_WAVES
@@ -253,7 +283,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         acc = mfma32(wa.y, xb.y, acc);
         acc = mfma32(wa.z, xb.z, acc);
         acc = mfma32(wa.w, xb.w, acc);
-        store_rows_tanh(&sH1[r][32 * jb], acc, hf);
+        store_rows_tanh<SPLIT>(&sH1[r][32 * jb], acc, hf);
       }
     }
     __syncthreads();
@@ -278,7 +308,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
           const BF8 al = __builtin_bit_cast(BF8, frags[frag_at(0, jb, st, 1, lane)]);
           acc = mfma_split(ah, al, bh[st], bl[st], acc);
         }
-        store_rows_tanh(&sH2[r][32 * jb], acc, hf);
+        store_rows_tanh<SPLIT>(&sH2[r][32 * jb], acc, hf);
       }
     } else {
       float hb[32];
@@ -298,7 +328,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         F16 acc = bias_frag(b2v + 32 * jb, hf);
 #pragma unroll
         for (int t = 0; t < 32; ++t) acc = mfma32(wa[t], hb[t], acc);
-        store_rows_tanh(&sH2[r][32 * jb], acc, hf);
+        store_rows_tanh<SPLIT>(&sH2[r][32 * jb], acc, hf);
       }
     }
     __syncthreads();
@@ -326,7 +356,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
           for (int o = 1; o < 8; ++o) m = fmaxf(m, z[o]);
           float se = 0.f;
 #pragma unroll
-          for (int o = 0; o < 8; ++o) se += expf(z[o] - m);
+          for (int o = 0; o < 8; ++o) se += exp_of<SPLIT>(z[o] - m);
           const int act = actions[srow];
           float za = z[0];
 #pragma unroll
@@ -384,7 +414,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
           z[v] = q4 ? rcv[v] : own[v];
           z[4 + v] = q4 ? own[v] : rcv[v];
         }
-        actor_loss(z, tail, valid, c, g3, pg_sum, ent_sum);
+        actor_loss<SPLIT>(z, tail, valid, c, g3, pg_sum, ent_sum);
 #pragma unroll
         for (int o = 0; o < 8; ++o) dB3[o] += g3[o];
         *reinterpret_cast<float4*>(&sG3[lane][0]) = make_float4(g3[0], g3[1], g3[2], g3[3]);
