@@ -2199,14 +2199,15 @@ static bool one_lane_prio(int n_envs) {
 // (Pre / prepare_request): at one wave per SIMD, where no partner wave issues in that LDS wait
 // (DESIGN.md section 5); same-step auto-reset only (no tick is a next-step reset burst).
 // FOOTSIES_PREFETCH=0 / 1 forces it off / on (A/B timing, and the parity suite runs both).
-static bool request_prefetch(const StepParams& p) {
+// (row_launch: a fused launch over action rows -- not the in-kernel actor's, not hashed actions)
+static bool request_prefetch(bool row_launch, int autoreset_mode, bool geom, int n_steps, int n_envs) {
   static const int forced = [] {
     const char* e = getenv("FOOTSIES_PREFETCH");
     return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' + 1 : 0;
   }();
-  if (p.autoreset_mode != FS_AUTORESET_SAME_STEP || p.geom || p.pol.w1 || !p.p1 || p.n_steps < 2) return false;
+  if (!row_launch || autoreset_mode != FS_AUTORESET_SAME_STEP || geom || n_steps < 2) return false;
   if (forced) return forced == 2;
-  return !two_waves_per_simd(p.n_envs);
+  return !two_waves_per_simd(n_envs);
 }
 
 template <int FM, int P2>
@@ -2214,7 +2215,7 @@ static void launch_step_p2(const StepParams& p_in, hipStream_t s) {
   const dim3 grid = grid_for(2 * p_in.n_envs), block(kBlock);
   StepParams p = p_in;
   p.prio = two_waves_per_simd(p.n_envs);
-  p.prefetch = P2 != kActors && request_prefetch(p);
+  p.prefetch = P2 != kActors && request_prefetch(!p.pol.w1 && p.p1, p.autoreset_mode, p.geom, p.n_steps, p.n_envs);
   if (p.pol.w1) hipLaunchKernelGGL((k_step_n_policy<FM, P2>), grid, block, 0, s, p);
   else if (p.out.pk_lanes) {  // (rows: fs_api checks)
     if constexpr (P2 != kActors) {
@@ -2270,13 +2271,7 @@ const char* step_kernel_name(bool policy, bool hashed, int n_steps, int n_envs, 
                              bool packed, int autoreset_mode) {
   static thread_local char buf[64];
   const bool one = !policy && !hashed && variant != kActors && !geom && fused_one_lane(n_envs, variant, packed);
-  StepParams q{};  // the prefetch test of launch_step_p2 for a row launch of this shape
-  q.autoreset_mode = autoreset_mode;
-  q.geom = geom;
-  q.n_steps = n_steps;
-  q.n_envs = n_envs;
-  q.p1 = reinterpret_cast<const uint8_t*>(1);
-  const bool pf = !policy && !hashed && !one && variant != kActors && request_prefetch(q);
+  const bool pf = !one && variant != kActors && request_prefetch(!policy && !hashed, autoreset_mode, geom, n_steps, n_envs);
   const char* k = policy ? "k_step_n_policy" : packed ? (one ? "k_step_n1_packed" : pf ? "k_step_n_packed_pf" : "k_step_n_packed")
                 : hashed ? "k_step_n_hashed" : n_steps == 1 ? "k_step" : one ? "k_step_n1" : pf ? "k_step_n_pf" : "k_step_n";
   snprintf(buf, sizeof buf, "fsk::%s<%d, %d>", k, float_mode == FS_FLOAT_DOUBLE ? 1 : 0, variant);
