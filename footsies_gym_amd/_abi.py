@@ -6,7 +6,7 @@ the test-side oracle binding (``oracle/binding.py``) agree on layouts.
 """
 import ctypes as C
 
-FS_ABI_VERSION = 5
+FS_ABI_VERSION = 6
 
 FS_OK = 0
 FS_E_INVALID = -1
@@ -170,6 +170,9 @@ LIB_FUNCTIONS = {
                               C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "fs_ppo_grad_ex": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp), C.c_float, C.c_float,
                                  C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]),
+    "fs_ppo_grad_runs": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.POINTER(fs_mlp),
+                                   C.POINTER(fs_mlp), C.c_float, C.c_float, C.c_float, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]),
     "fs_ppo_eval_ex": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(fs_mlp), C.POINTER(fs_mlp),
                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]),
     "fs_ppo_gae": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_float,

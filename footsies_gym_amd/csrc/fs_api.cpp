@@ -548,9 +548,10 @@ FS_API int fs_step_n_policy(fs_handle h, int n, const fs_policy* pol, const uint
 
 FS_API size_t fs_ppo_workspace_bytes(void) { return fsk::ppo_workspace_bytes(); }
 
-FS_API int fs_ppo_grad_ex(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
-                          float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
-                          size_t workspace_bytes, void* stream, int precision) {
+static int ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
+                    float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
+                    size_t workspace_bytes, void* stream, int precision, const int64_t* runs = nullptr,
+                    int run_shift = 0, int64_t n_rows = 0) {
   if (!rows || n <= 0 || !actor || !critic || !grad_out || !loss_out || !workspace)
     return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: rows, n > 0, both networks, outputs and workspace required");
   if (workspace_bytes < fsk::ppo_workspace_bytes())
@@ -565,9 +566,31 @@ FS_API int fs_ppo_grad_ex(const float* rows, int64_t n, const fs_mlp* actor, con
   for (int i = 0; i < 6; ++i)
     if (!a[i] || !c[i]) return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad: all six arrays of each network required");
   const hipError_t e = fsk::launch_ppo_grad(rows, n, a, c, clip, vf_coef, ent_coef, grad_out, loss_out, workspace,
-                                            static_cast<hipStream_t>(stream), precision == FS_PPO_SPLIT_BF16);
+                                            static_cast<hipStream_t>(stream), precision == FS_PPO_SPLIT_BF16, runs,
+                                            run_shift, n_rows);
   if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_ppo_grad: %s", hipGetErrorString(e));
   return FS_OK;
+}
+
+FS_API int fs_ppo_grad_ex(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
+                          float vf_coef, float ent_coef, float* grad_out, float* loss_out, void* workspace,
+                          size_t workspace_bytes, void* stream, int precision) {
+  return ppo_grad(rows, n, actor, critic, clip, vf_coef, ent_coef, grad_out, loss_out, workspace, workspace_bytes,
+                  stream, precision);
+}
+
+FS_API int fs_ppo_grad_runs(const float* rows, int64_t n_rows, const int64_t* runs, int64_t n_runs, int run_shift,
+                            const fs_mlp* actor, const fs_mlp* critic, float clip, float vf_coef, float ent_coef,
+                            float* grad_out, float* loss_out, void* workspace, size_t workspace_bytes, void* stream,
+                            int precision) {
+  if (!runs || n_runs <= 0 || n_rows <= 0 || run_shift < 0 || run_shift > 30)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad_runs: runs, n_runs > 0, n_rows > 0 and run_shift in [0, 30] "
+                                          "required");
+  if (n_runs > (INT64_MAX >> run_shift) || (n_rows >> run_shift) < 1)
+    return set_err(nullptr, FS_E_INVALID, "fs_ppo_grad_runs: %lld runs of 2^%d rows do not fit a %lld-row table",
+                   (long long)n_runs, run_shift, (long long)n_rows);
+  return ppo_grad(rows, n_runs << run_shift, actor, critic, clip, vf_coef, ent_coef, grad_out, loss_out, workspace,
+                  workspace_bytes, stream, precision, runs, run_shift, n_rows);
 }
 
 FS_API int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,

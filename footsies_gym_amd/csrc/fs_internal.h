@@ -147,7 +147,8 @@ hipError_t launch_pack_records(const DevOutputs& o, void* dst, int n, hipStream_
 size_t ppo_workspace_bytes();
 hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
                            float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
-                           hipStream_t s, bool split);
+                           hipStream_t s, bool split, const int64_t* runs = nullptr, int run_shift = 0,
+                           int64_t n_rows = 0);
 hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp,
                            const float* const actor[6], const float* const critic[6], float* values, float* logp,
                            void* workspace, hipStream_t s, bool split);

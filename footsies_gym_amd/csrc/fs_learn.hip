@@ -228,7 +228,9 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
                                                          Coef c, float* __restrict__ partial,
                                                          const uint8_t* __restrict__ actions = nullptr,
                                                          const float* __restrict__ w2t = nullptr,
-                                                         const uint4* __restrict__ frags = nullptr) {
+                                                         const uint4* __restrict__ frags = nullptr,
+                                                         const int64_t* __restrict__ runs = nullptr, int run_shift = 0,
+                                                         int64_t n_rows = 0) {
   constexpr int kStride = EVAL ? kF : kRow;
   __shared__ float sX[kTile][kF];
   __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample, then g1
@@ -246,7 +248,16 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 #pragma unroll
   for (int o = 0; o < OUT; ++o) dW3[o] = dB3[o] = 0.f;
 
+  // (runs: sample i of the minibatch is row runs[i >> run_shift] * 2^run_shift + i mod 2^run_shift of
+  // the table, fs_ppo_grad_runs; each lane's run entry is read one tile ahead)
+  auto run_of = [&](int64_t t) -> int64_t {
+    const int64_t i = t * kTile + lane;
+    return (runs && lane < kTile && t < tiles && i < n) ? runs[i >> run_shift] : 0;
+  };
+  int64_t run_next = run_of(blockIdx.x);
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t run_cur = run_next;
+    run_next = run_of(tile + gridDim.x);
     // weights re-read every tile (L1 / scalar-cache hits): hoisted out of the loop they would
     // hold ~200 registers; W3 / B3 as wave-uniform scalar loads (constant address space)
     const float *w1v = w1, *b1v = b1, *w2v = w2, *b2v = b2, *w3v = w3, *b3v = b3, *w2tv = w2t;
@@ -254,12 +265,19 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     const CPtr W3 = (CPtr)w3v, B3 = (CPtr)b3v;
     const int64_t left = n - tile * kTile;
     const int ns = (int)(left < kTile ? left : kTile);
-    const bool valid = lane < ns;  // rows past n: x = 0 and g3 = 0, so they add nothing
+    int64_t row = tile * kTile + lane;
+    bool in_table = true;
+    if (runs) {  // (a run entry outside the table reads nothing and adds nothing, as a padding row)
+      const int64_t mask = ((int64_t)1 << run_shift) - 1;
+      row = (run_cur << run_shift) | (row & mask);
+      in_table = run_cur >= 0 && row < n_rows;
+    }
+    const bool valid = lane < ns && in_table;  // rows past n: x = 0 and g3 = 0, so they add nothing
 
     // ---- rows -> x (LDS) and the loss inputs (registers of lanes < kTile) --------------------
     float tail[4] = {0.f, 0.f, 0.f, 0.f};
     if (lane < kTile) {
-      const float4* rp = reinterpret_cast<const float4*>(rows + (tile * kTile + (valid ? lane : 0)) * kStride);
+      const float4* rp = reinterpret_cast<const float4*>(rows + (valid ? row : 0) * kStride);
       float4 r0 = rp[0], r1 = rp[1];
       if constexpr (!EVAL) {
         const float4 r2 = rp[2];
@@ -797,7 +815,7 @@ size_t ppo_workspace_bytes() { return ppo_frag_offset() + sizeof(uint4) * 2 * fs
 
 hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
                            float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
-                           hipStream_t s, bool split) {
+                           hipStream_t s, bool split, const int64_t* runs, int run_shift, int64_t n_rows) {
   using namespace fsl;
   const int64_t tiles = (n + kTile - 1) / kTile;
   const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
@@ -811,15 +829,16 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
   if (split) {
     hipLaunchKernelGGL(k_ppo_frag, dim3(8), dim3(256), 0, s, actor[2], critic[2], frags);
     hipLaunchKernelGGL((k_ppo_grad<8, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1],
-                       actor[2], actor[3], actor[4], actor[5], c, pa, nullptr, nullptr, frags);
+                       actor[2], actor[3], actor[4], actor[5], c, pa, nullptr, nullptr, frags, runs, run_shift, n_rows);
     hipLaunchKernelGGL((k_ppo_grad<1, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1],
-                       critic[2], critic[3], critic[4], critic[5], c, pc, nullptr, nullptr, frags + kFragsPerNet);
+                       critic[2], critic[3], critic[4], critic[5], c, pc, nullptr, nullptr, frags + kFragsPerNet, runs, run_shift,
+                       n_rows);
   } else {
     hipLaunchKernelGGL(k_ppo_t64, dim3(4, 2), dim3(256), 0, s, actor[2], critic[2], w2t);
     hipLaunchKernelGGL(k_ppo_grad<8>, dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1], actor[2],
-                       actor[3], actor[4], actor[5], c, pa, nullptr, w2t);
+                       actor[3], actor[4], actor[5], c, pa, nullptr, w2t, nullptr, runs, run_shift, n_rows);
     hipLaunchKernelGGL(k_ppo_grad<1>, dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1], critic[2],
-                       critic[3], critic[4], critic[5], c, pc, nullptr, w2t + kH * kH);
+                       critic[3], critic[4], critic[5], c, pc, nullptr, w2t + kH * kH, nullptr, runs, run_shift, n_rows);
   }
   hipLaunchKernelGGL(k_ppo_reduce<8>, dim3((n_params<8>() + 3 + 63) / 64), dim3(1024), 0, s, pa, waves, grad, loss,
                      c.inv_n);

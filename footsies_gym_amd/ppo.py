@@ -225,17 +225,29 @@ class PPOGrad:
                                    prec))
         return values, logp
 
-    def __call__(self, rows, clip, vf_coef, ent_coef):
-        """rows: device [n][12] fp32 (features, action, old log-prob, advantage, return)."""
+    def __call__(self, rows, clip, vf_coef, ent_coef, runs=None, run_len=1):
+        """rows: device [n][12] fp32 (features, action, old log-prob, advantage, return).  With
+        `runs` (device int64 [k]) the minibatch is the k runs rows[runs[j] * run_len :
+        (runs[j] + 1) * run_len] in that order, read in place (fs_ppo_grad_runs; run_len a power
+        of two): the same gradient, bit for bit, as on ``rows.view(-1, run_len, 12)[runs]``."""
         torch = _torch()
         if rows.dtype != torch.float32 or rows.dim() != 2 or rows.shape[1] != 12 or not rows.is_contiguous():
             raise ValueError("rows must be a contiguous [n, 12] float32 tensor")
         self._check_bindings()
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        check(lib().fs_ppo_grad_ex(C.c_void_p(rows.data_ptr()), rows.shape[0], C.byref(self._mlps[0]),
-                                   C.byref(self._mlps[1]), clip, vf_coef, ent_coef, C.c_void_p(self.grad.data_ptr()),
-                                   C.c_void_p(self.loss.data_ptr()), C.c_void_p(self.workspace.data_ptr()),
-                                   self.workspace.numel(), C.c_void_p(stream), self._prec))
+        tail = (C.byref(self._mlps[0]), C.byref(self._mlps[1]), clip, vf_coef, ent_coef,
+                C.c_void_p(self.grad.data_ptr()), C.c_void_p(self.loss.data_ptr()),
+                C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), C.c_void_p(stream), self._prec)
+        if runs is None:
+            check(lib().fs_ppo_grad_ex(C.c_void_p(rows.data_ptr()), rows.shape[0], *tail))
+            return self.loss
+        shift = int(run_len).bit_length() - 1
+        if run_len < 1 or (1 << shift) != run_len:
+            raise ValueError("run_len must be a power of two")
+        if runs.dtype != torch.int64 or runs.dim() != 1 or not runs.is_contiguous() or runs.device != rows.device:
+            raise ValueError("runs must be a contiguous int64 vector on the rows' device")
+        check(lib().fs_ppo_grad_runs(C.c_void_p(rows.data_ptr()), rows.shape[0], C.c_void_p(runs.data_ptr()),
+                                     runs.numel(), shift, *tail))
         return self.loss
 
 
@@ -420,11 +432,11 @@ class PPOTrainer:
         for _ in range(self.epochs):
             perm = torch.randperm(M // C, device=x.device, generator=self.gen)
             for i in range(0, M // C, nb):
-                b = runs[perm[i:i + nb]].view(-1, rows.shape[1])
-                if self._grad is not None:  # fused forward + backward straight into .grad
-                    lm = self._grad(b, self.clip, self.vf_coef, self.ent_coef)
+                if self._grad is not None:  # fused forward + backward straight into .grad, the runs read in place
+                    lm = self._grad(rows, self.clip, self.vf_coef, self.ent_coef, runs=perm[i:i + nb], run_len=C)
                     self.opt.step()
                     continue
+                b = runs[perm[i:i + nb]].view(-1, rows.shape[1])
                 xb, ab = b[:, :N_FEATURES], b[:, N_FEATURES].long()
                 oldb, advb, retb = b[:, N_FEATURES + 1], b[:, N_FEATURES + 2], b[:, N_FEATURES + 3]
                 logits = mlp(self.actor, xb)

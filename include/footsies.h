@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 5
+#define FS_ABI_VERSION 6
 
 /* error codes */
 #define FS_OK 0
@@ -338,8 +338,9 @@ int fs_ppo_grad(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp*
  * MFMA, exact fp32 products) or FS_PPO_SPLIT_BF16 (each fp32 operand split into a bf16 hi + lo
  * pair and the product taken as hi.hi + hi.lo + lo.hi on bf16 MFMA with fp32 accumulation:
  * relative error per product below 2^-15, ~5x less matrix-pipe time).  The layers with 8 inputs
- * or outputs stay fp32.  fs_ppo_eval_ex needs the workspace for FS_PPO_SPLIT_BF16 (NULL / 0 for
- * FS_PPO_FP32); a workspace is not shared between calls in flight on different streams. */
+ * or outputs stay fp32; FS_PPO_SPLIT_BF16 takes tanh and exp from the hardware exp2 / reciprocal
+ * (tanh within 2.5e-7 absolutely).  fs_ppo_eval_ex needs the workspace for FS_PPO_SPLIT_BF16 (NULL / 0
+ * for FS_PPO_FP32); a workspace is not shared between calls in flight on different streams. */
 #define FS_PPO_FP32 0
 #define FS_PPO_SPLIT_BF16 1
 int fs_ppo_grad_ex(const float* rows, int64_t n, const fs_mlp* actor, const fs_mlp* critic, float clip,
@@ -348,6 +349,17 @@ int fs_ppo_grad_ex(const float* rows, int64_t n, const fs_mlp* actor, const fs_m
 int fs_ppo_eval_ex(const float* x, int64_t n_values, const uint8_t* actions, int64_t n_logp, const fs_mlp* actor,
                    const fs_mlp* critic, float* values_out, float* logp_out, void* workspace, size_t workspace_bytes,
                    void* stream, int precision);
+/* fs_ppo_grad_ex over a minibatch of whole runs of the [n_rows][12] table, without gathering it
+ * first (ppo.py PPOTrainer.update: runs of consecutive samples in a shuffled order): sample i of
+ * the minibatch is row runs[i >> run_shift] * 2^run_shift + (i mod 2^run_shift), for
+ * i < n_runs * 2^run_shift; runs: device int64 [n_runs].  Same results, bit for bit, as
+ * fs_ppo_grad_ex on those rows gathered in that order.  A run entry whose rows fall outside the
+ * table is read as a padding row (nothing read, nothing added; the mean still counts it): the
+ * entries are device data, so they are not checked on the host.  (ABI 6.) */
+int fs_ppo_grad_runs(const float* rows, int64_t n_rows, const int64_t* runs, int64_t n_runs, int run_shift,
+                     const fs_mlp* actor, const fs_mlp* critic, float clip, float vf_coef, float ent_coef,
+                     float* grad_out, float* loss_out, void* workspace, size_t workspace_bytes, void* stream,
+                     int precision);
 /* GAE of a [T][N] trajectory (ppo.py gae), asynchronously on `stream`: rewards device
  * [T][N] f64 and done device [T][N] u8 as fs_step_n_policy's trajectory holds them, values
  * device [T + 1][N] f32 (the last row bootstraps); delta = (r + (gamma v[t+1]) keep) - v[t],

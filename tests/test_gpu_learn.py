@@ -120,6 +120,41 @@ def test_ppo_grad_is_deterministic_and_rejects_bad_input(precision):
         PPOGrad(actor, critic, precision="bf16")
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("run_len,n_runs", [(2048, 37), (1, 5001), (16, 333)])
+def test_ppo_grad_over_runs_equals_gathered_rows(precision, run_len, n_runs):
+    """fs_ppo_grad_runs (PPOTrainer.update's minibatches: shuffled runs of consecutive samples read
+    in place) against fs_ppo_grad_ex on the same runs gathered into a table first: the gradient and
+    the loss means bit for bit -- run lengths of whole tiles (2048, PPOTrainer's), single samples
+    and runs shorter than a tile (16), with a partial last tile; then out-of-table run entries
+    read as padding rows and the host-side argument checks."""
+    import torch
+    from footsies_gym_amd._lib import FootsiesError
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=3)
+    total = 64 * 2048
+    rows = _rows(actor, total, seed=11)
+    g = torch.Generator(device="cuda").manual_seed(run_len + n_runs)
+    runs = torch.randperm(total // run_len, generator=g, device="cuda")[:n_runs].contiguous()
+    pg = PPOGrad(actor, critic, precision=precision)
+    gathered = rows.view(-1, run_len, 12)[runs].reshape(-1, 12).contiguous()
+    loss_g = pg(gathered, 0.2, 0.5, 0.01).clone()
+    grad_g = pg.grad.clone()
+    loss_r = pg(rows, 0.2, 0.5, 0.01, runs=runs, run_len=run_len).clone()
+    assert torch.equal(grad_g, pg.grad) and torch.equal(loss_g, loss_r)
+    # a run entry past the table: nothing read, nothing added (the padding rows' zero gradient)
+    bad = runs.clone()
+    bad[-1] = total // run_len + 5
+    pg(rows, 0.2, 0.5, 0.01, runs=bad, run_len=run_len)
+    assert bool(torch.isfinite(pg.grad).all())
+    with pytest.raises(ValueError):
+        pg(rows, 0.2, 0.5, 0.01, runs=runs, run_len=3)
+    with pytest.raises(ValueError):
+        pg(rows, 0.2, 0.5, 0.01, runs=runs.int(), run_len=run_len)
+    with pytest.raises(FootsiesError):
+        pg(rows, 0.2, 0.5, 0.01, runs=runs[:0], run_len=run_len)
+
+
 def test_ppo_trainer_hip_step_equals_torch_step():
     """One minibatch update through PPOTrainer's two learners from the same weights and rows:
     the parameters after Adam agree (Adam's first step moves each weight by ~lr * sign(grad), so
