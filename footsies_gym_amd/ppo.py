@@ -199,10 +199,11 @@ class PPOGrad:
         if moved:
             self._bind()
 
-    def evaluate(self, x, actions=None, n_logp=0, precision=None):
+    def evaluate(self, x, actions=None, n_logp=0, precision=None, values=True):
         """fs_ppo_eval: (critic(x) [n], log_softmax(actor(x[:n_logp]))[actions] [n_logp] or None),
         without gradient; x: device [n, 8] fp32, actions: device uint8 [n_logp].  `precision`:
-        "fp32" or "split_bf16" for this call (default: the learner's own)."""
+        "fp32" or "split_bf16" for this call (default: the learner's own); values=False: the
+        log-probs only (the critic is not run, the first result is None)."""
         torch = _torch()
         if precision is not None and precision not in self.PRECISIONS:
             raise ValueError("precision must be one of %s" % sorted(self.PRECISIONS))
@@ -210,7 +211,8 @@ class PPOGrad:
         if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES or not x.is_contiguous():
             raise ValueError("x must be a contiguous [n, 8] float32 tensor")
         n = x.shape[0]
-        values = torch.empty(n, dtype=torch.float32, device=x.device)
+        want_values = values
+        values = torch.empty(n, dtype=torch.float32, device=x.device) if want_values else None
         logp = None
         if n_logp:
             if actions is None or actions.dtype != torch.uint8 or actions.numel() < n_logp or not actions.is_contiguous():
@@ -220,7 +222,8 @@ class PPOGrad:
         stream = torch.cuda.current_stream(self.device).cuda_stream
         check(lib().fs_ppo_eval_ex(C.c_void_p(x.data_ptr()), n, C.c_void_p(actions.data_ptr() if n_logp else None),
                                    n_logp, C.byref(self._mlps[0]), C.byref(self._mlps[1]),
-                                   C.c_void_p(values.data_ptr()), C.c_void_p(logp.data_ptr() if n_logp else None),
+                                   C.c_void_p(values.data_ptr() if want_values else None),
+                                   C.c_void_p(logp.data_ptr() if n_logp else None),
                                    C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), C.c_void_p(stream),
                                    prec))
         return values, logp
@@ -409,7 +412,7 @@ class PPOTrainer:
                     v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk, precision="fp32")
                 else:
                     v, _ = self._grad.evaluate(feats.view(-1, N_FEATURES))
-                    _, old32 = self._grad.evaluate(x[:nk].contiguous(), a, nk, precision="fp32")
+                    _, old32 = self._grad.evaluate(x[:nk].contiguous(), a, nk, precision="fp32", values=False)
                 values = v.view(T + 1, N)
                 adv, ret = gae_device(rewards, dones, values, self.gamma, self.lam)
                 old = behav if self.old_logp == "behaviour" else old32

@@ -325,3 +325,19 @@ def test_eval_precision_override_is_the_fp32_path():
     assert torch.equal(v, v32) and torch.equal(lp, lp32)
     with pytest.raises(ValueError):
         split.evaluate(x, a, n, precision="bf16")
+
+
+def test_eval_log_probs_without_the_critic():
+    """evaluate(values=False) -- PPOTrainer.update's fp32 reference log-probs -- runs only the actor
+    (fs_ppo_eval with values_out NULL): the same log-probs, bit for bit, as the call with values."""
+    import torch
+    from footsies_gym_amd.ppo import PPOGrad
+    actor, critic = _nets(seed=4)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.rand((5000, 8), generator=g, device="cuda")
+    a = torch.randint(0, 8, (5000,), generator=g, device="cuda").to(torch.uint8)
+    for precision in PRECISIONS:
+        pg = PPOGrad(actor, critic, precision=precision)
+        v, lp = pg.evaluate(x, a, 3001)
+        none, lp2 = pg.evaluate(x, a, 3001, values=False)
+        assert none is None and v.shape == (5000,) and torch.equal(lp, lp2)
