@@ -34,6 +34,7 @@ constexpr int kPad = kH + 4;   // LDS row stride of the h1 / h2 stages (b128 wri
 // results, the output layer's two 16-column blocks) are written for it
 constexpr int kTile = 32;        // (lanes >= kTile idle in the per-sample phases)
 constexpr int kMaxWaves = 2048;  // grid cap: two waves per SIMD
+constexpr int kMaxEvalWaves = 4096;  // the forward pass alone: four (fewer registers, ~10 KB of LDS)
 
 template <int OUT>
 constexpr int n_params() { return kH * kF + kH + kH * kH + kH + OUT * kH + OUT; }
@@ -234,8 +235,11 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
   constexpr int kStride = EVAL ? kF : kRow;
   __shared__ float sX[kTile][kF];
   __shared__ float sH1[kTile][kPad];  // rows: h1 of each sample, then g1
-  __shared__ float sH2[kTile][kPad];  // rows: h2, then g2
-  __shared__ float sG3[kTile][8];
+  // (the forward pass alone keeps h2 in h1's stage -- layer 2 reads all of h1 into registers before
+  // it writes -- so its blocks need ~10 KB of LDS and four of them fit per SIMD)
+  __shared__ float sH2[EVAL ? 1 : kTile][kPad];  // rows: h2, then g2
+  __shared__ float sG3[EVAL ? 1 : kTile][8];
+  float (*const H2)[kPad] = EVAL ? sH1 : sH2;
 
   const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
   F16 dW2[2][2];  // dW2 as four 32 x 32 MFMA accumulators [i block][k block]
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
           const BF8 al = __builtin_bit_cast(BF8, frags[frag_at(0, jb, st, 1, lane)]);
           acc = mfma_split(ah, al, bh[st], bl[st], acc);
         }
-        store_rows_tanh<SPLIT>(&sH2[r][32 * jb], acc, hf);
+        store_rows_tanh<SPLIT>(&H2[r][32 * jb], acc, hf);
       }
     } else {
       float hb[32];
@@ -346,7 +350,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         F16 acc = bias_frag(b2v + 32 * jb, hf);
 #pragma unroll
         for (int t = 0; t < 32; ++t) acc = mfma32(wa[t], hb[t], acc);
-        store_rows_tanh<SPLIT>(&sH2[r][32 * jb], acc, hf);
+        store_rows_tanh<SPLIT>(&H2[r][32 * jb], acc, hf);
       }
     }
     __syncthreads();
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         float hv[kH];
 #pragma unroll
         for (int k = 0; k < kH; k += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(&sH2[lane][k]);
+          const float4 v = *reinterpret_cast<const float4*>(&H2[lane][k]);
           hv[k] = v.x; hv[k + 1] = v.y; hv[k + 2] = v.z; hv[k + 3] = v.w;
         }
         const int64_t srow = tile * kTile + lane;
@@ -412,7 +416,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         float hz[16];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float4 v = *reinterpret_cast<const float4*>(&sH2[16 * nb + c16][16 * q4 + 4 * u]);
+          const float4 v = *reinterpret_cast<const float4*>(&H2[16 * nb + c16][16 * q4 + 4 * u]);
           hz[4 * u] = v.x; hz[4 * u + 1] = v.y; hz[4 * u + 2] = v.z; hz[4 * u + 3] = v.w;
         }
         F4 acc = {bz.x, bz.y, bz.z, bz.w};
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       float h2[kH];
 #pragma unroll
       for (int k = 0; k < kH; k += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(&sH2[lane][k]);
+        const float4 v = *reinterpret_cast<const float4*>(&H2[lane][k]);
         h2[k] = v.x; h2[k + 1] = v.y; h2[k + 2] = v.z; h2[k + 3] = v.w;
       }
       float v = B3[0];
@@ -459,7 +463,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 
     // ---- (lane = unit j) dW3's column j from h2's column and g3's rows -------------------------
     for (int t = 0; t < ns; ++t) {
-      const float h2c = sH2[t][lane];
+      const float h2c = H2[t][lane];
 #pragma unroll
       for (int o = 0; o < OUT; ++o) dW3[o] = fmaf(sG3[t][o], h2c, dW3[o]);
     }
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         for (int t = 0; t < 4; ++t) acc = mfma32(w3v[(t + 4 * hf) * kH + 32 * jb + r], gb[t], acc);
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          float4* hp = reinterpret_cast<float4*>(&sH2[r][32 * jb + 8 * qq + 4 * hf]);
+          float4* hp = reinterpret_cast<float4*>(&H2[r][32 * jb + 8 * qq + 4 * hf]);
           const float4 hv = *hp;
           *hp = make_float4(acc[4 * qq] * (1.f - hv.x * hv.x), acc[4 * qq + 1] * (1.f - hv.y * hv.y),
                             acc[4 * qq + 2] * (1.f - hv.z * hv.z), acc[4 * qq + 3] * (1.f - hv.w * hv.w));
@@ -495,7 +499,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         for (int qq = 0; qq < 4; ++qq) {
           const int j = 32 * jb + 8 * qq + 4 * hf;
           const float4 w = *reinterpret_cast<const float4*>(&w3v[j]);
-          float4* hp = reinterpret_cast<float4*>(&sH2[r][j]);
+          float4* hp = reinterpret_cast<float4*>(&H2[r][j]);
           const float4 hv = *hp;
           *hp = make_float4(fmaf(w.x, g3, 0.f) * (1.f - hv.x * hv.x), fmaf(w.y, g3, 0.f) * (1.f - hv.y * hv.y),
                             fmaf(w.z, g3, 0.f) * (1.f - hv.z * hv.z), fmaf(w.w, g3, 0.f) * (1.f - hv.w * hv.w));
@@ -513,7 +517,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         for (int ib = 0; ib < 2; ++ib) {
           float v[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = sH2[16 * st + 8 * hf + j][32 * ib + r];
+          for (int j = 0; j < 8; ++j) v[j] = H2[16 * st + 8 * hf + j][32 * ib + r];
 #pragma unroll
           for (int j = 0; j < 8; ++j) dB2[ib] += v[j];
           split8(v, ah[ib], al[ib]);
@@ -534,7 +538,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 #pragma unroll
     for (int t = 0; t < kTile / 2; ++t) {
       const int sidx = t + (kTile / 2) * hf;
-      const float a0 = sH2[sidx][r], a1 = sH2[sidx][32 + r];
+      const float a0 = H2[sidx][r], a1 = H2[sidx][32 + r];
       const float h0 = sH1[sidx][r], h1v = sH1[sidx][32 + r];
       dB2[0] += a0;
       dB2[1] += a1;
@@ -552,8 +556,8 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       BF8 gh[4], gl[4];
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
-        const float4 v0 = *reinterpret_cast<const float4*>(&sH2[r][16 * st + 8 * hf]);
-        const float4 v1 = *reinterpret_cast<const float4*>(&sH2[r][16 * st + 8 * hf + 4]);
+        const float4 v0 = *reinterpret_cast<const float4*>(&H2[r][16 * st + 8 * hf]);
+        const float4 v1 = *reinterpret_cast<const float4*>(&H2[r][16 * st + 8 * hf + 4]);
         const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         split8(v, gh[st], gl[st]);
       }
@@ -580,7 +584,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       float gb[32];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float4 v = *reinterpret_cast<const float4*>(&sH2[r][32 * hf + 4 * u]);
+        const float4 v = *reinterpret_cast<const float4*>(&H2[r][32 * hf + 4 * u]);
         gb[4 * u] = v.x; gb[4 * u + 1] = v.y; gb[4 * u + 2] = v.z; gb[4 * u + 3] = v.w;
       }
 #pragma unroll 1
@@ -861,7 +865,7 @@ hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* acti
   }
   if (run_v) {
     const int64_t tiles = (n_values + kTile - 1) / kTile;
-    const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
+    const int waves = (int)(tiles < kMaxEvalWaves ? tiles : kMaxEvalWaves);
     if (split)
       hipLaunchKernelGGL((k_ppo_grad<1, true, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, critic[0],
                          critic[1], critic[2], critic[3], critic[4], critic[5], c, values, nullptr, nullptr,
@@ -872,7 +876,7 @@ hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* acti
   }
   if (run_l) {
     const int64_t tiles = (n_logp + kTile - 1) / kTile;
-    const int waves = (int)(tiles < kMaxWaves ? tiles : kMaxWaves);
+    const int waves = (int)(tiles < kMaxEvalWaves ? tiles : kMaxEvalWaves);
     if (split)
       hipLaunchKernelGGL((k_ppo_grad<8, true, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, actor[0],
                          actor[1], actor[2], actor[3], actor[4], actor[5], c, logp, actions, nullptr, frags);
