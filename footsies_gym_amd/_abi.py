@@ -195,6 +195,9 @@ LIB_FUNCTIONS = {
     "fs_step_kernel": (C.c_char_p, [C.c_void_p, C.c_int, C.c_int]),
     "fs_host_convert": (C.c_int, [C.POINTER(fs_outputs), C.c_int64, C.c_void_p, C.c_int64, C.POINTER(fs_host_arrays),
                                   C.c_int]),
+    "fs_host_convert_start": (C.c_int, [C.POINTER(fs_outputs), C.c_int64, C.c_void_p, C.c_int64,
+                                        C.POINTER(fs_host_arrays), C.c_int]),
+    "fs_host_convert_wait": (C.c_int, []),
     "fs_destroy": (None, [C.c_void_p]),
     "fs_last_error": (C.c_char_p, [C.c_void_p]),
 }

@@ -928,8 +928,8 @@ class HostPool {
 };
 }  // namespace
 
-FS_API int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n,
-                           const fs_host_arrays* dst, int threads) {
+static int host_convert_check(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n,
+                              const fs_host_arrays* dst) {
   if (!src || !dst || n < 0 || n_src < 0)
     return set_err(nullptr, FS_E_INVALID, "fs_host_convert: src, dst, n >= 0 and n_src >= 0 required");
   if (!rows && n > n_src) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: n exceeds the source's n_src rows");
@@ -937,8 +937,8 @@ FS_API int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* 
     for (int64_t i = 0; i < n; ++i)
       if (rows[i] < 0 || rows[i] >= n_src)
         return set_err(nullptr, FS_E_INVALID, "fs_host_convert: rows[i] outside [0, n_src)");
-  const fs_outputs S = *src;
-  const fs_host_arrays D = *dst;
+  const fs_outputs& S = *src;
+  const fs_host_arrays& D = *dst;
   if ((D.guard || D.info_guard) && !S.guard) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: no guard source");
   if ((D.move || D.info_move) && !S.move) return set_err(nullptr, FS_E_INVALID, "fs_host_convert: no move source");
   if ((D.move_frame || D.info_move_frame) && !S.move_frame)
@@ -949,6 +949,11 @@ FS_API int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* 
       ((D.p1_hitstun || D.p2_hitstun) && !S.hitstun) || (D.reward && !S.reward) ||
       (D.terminated && !S.terminated) || (D.truncated && !S.truncated))
     return set_err(nullptr, FS_E_INVALID, "fs_host_convert: a destination without its source");
+  return FS_OK;
+}
+
+// the conversion proper (arguments checked), on `threads` of the host pool
+static void host_convert_run(const fs_outputs S, const fs_host_arrays D, const int64_t* rows, int64_t n, int threads) {
   // below ~8k rows the threads' wake-up costs more than the conversion
   const int parts = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(threads, 1), n / 8192 + 1, 64}));
   HostPool::get().run(parts, [&](int part, int np) {
@@ -1003,5 +1008,77 @@ FS_API int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* 
       for (int64_t i = lo; i < hi; ++i) d[i] = sp[rows ? rows[i] : i] != 0;
     }
   });
+}
+
+FS_API int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n,
+                           const fs_host_arrays* dst, int threads) {
+  const int rc = host_convert_check(src, n_src, rows, n, dst);
+  if (rc) return rc;
+  host_convert_run(*src, *dst, rows, n, threads);
+  return FS_OK;
+}
+
+// fs_host_convert_start / _wait: one conversion at a time runs on a runner thread of its own (which
+// drives the host pool as fs_host_convert's caller would), while the caller goes on with other work;
+// a start while another thread's conversion is in flight waits for it first.
+class AsyncConvert {
+ public:
+  static AsyncConvert& get() {
+    static AsyncConvert* a = nullptr;
+    static pid_t owner = 0;
+    static std::mutex make;
+    std::lock_guard<std::mutex> g(make);
+    if (!a || owner != getpid()) {
+      a = new AsyncConvert();  // (one inherited through fork is abandoned, as the pool)
+      owner = getpid();
+    }
+    return *a;
+  }
+  void start(std::function<void()> job) {  // (after the conversion in flight, another thread's, ends)
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return !busy_; });
+    if (!runner_) runner_ = new std::thread([this] { loop(); });
+    job_ = std::move(job);
+    busy_ = true;
+    cv_.notify_one();
+  }
+  void wait() {  // until no conversion is in flight
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return !busy_; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [this] { return (bool)job_; });
+      std::function<void()> job = std::move(job_);
+      job_ = nullptr;
+      g.unlock();
+      job();
+      g.lock();
+      busy_ = false;
+      done_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  std::thread* runner_ = nullptr;
+  std::function<void()> job_;
+  bool busy_ = false;
+};
+
+FS_API int fs_host_convert_start(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n,
+                                 const fs_host_arrays* dst, int threads) {
+  const int rc = host_convert_check(src, n_src, rows, n, dst);
+  if (rc) return rc;
+  const fs_outputs S = *src;
+  const fs_host_arrays D = *dst;
+  AsyncConvert::get().start([S, D, rows, n, threads] { host_convert_run(S, D, rows, n, threads); });
+  return FS_OK;
+}
+
+FS_API int fs_host_convert_wait(void) {
+  AsyncConvert::get().wait();
   return FS_OK;
 }

@@ -139,6 +139,13 @@ def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
     fs_host_convert (one pass over the rows on the library's host threads).  info_copies=False:
     the info gets no observation entries (the caller shares the obs rows, see
     step_result_from_outputs)."""
+    obs, info, extra, _ = _host_convert_on(out, prefix, rows, n, want_step, info_copies, start=False)
+    return obs, info, extra
+
+
+def _host_convert_on(out, prefix, rows, n, want_step, info_copies=True, start=False):
+    """_host_convert; start=True returns as soon as the conversion runs on the library's threads
+    (fs_host_convert_start), with a fourth result to keep alive until fs_host_convert_wait."""
     so, keep = _src_struct(out, prefix, want_step)
     members = _DST_ROWS if want_step else (_DST_ROWS[:13] if info_copies else _DST_NO_COPIES)
     offs, totals = [], [0, 0, 0, 0, 0]
@@ -156,15 +163,15 @@ def _host_convert(out, prefix, rows, n, want_step, info_copies=True):
              for (name, dt, c, _), (b, off) in zip(members, offs)}
     r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
     n_src = len(out[prefix + "frame"])
-    check(lib().fs_host_convert(C.byref(so), n_src, None if r is None else r.ctypes.data, n, C.byref(dst),
-                                host_threads()))
-    del keep  # (the converted sources lived over the call)
+    convert = lib().fs_host_convert_start if start else lib().fs_host_convert
+    check(convert(C.byref(so), n_src, None if r is None else r.ctypes.data, n, C.byref(dst), host_threads()))
+    hold = (keep, r) if start else None  # (the converted sources and rows live until the wait)
     obs = {k: views[k] for k in ("guard", "move", "move_frame", "position")}
     info = {k: views[k] for k in ("frame", "p1_action", "p2_action", "p1_hitstun", "p2_hitstun")}
     if info_copies:
         info.update({k: views["info_" + k] for k in ("guard", "move", "move_frame", "position")})  # FE:379's copies
     extra = (views["reward"], views["terminated"], views["truncated"]) if want_step else None
-    return obs, info, extra
+    return obs, info, extra, hold
 
 
 def obs_info_from_outputs(out, prefix=""):
@@ -200,9 +207,23 @@ def obs_info_from_outputs_numpy(out, prefix=""):
 
 def step_result_from_outputs(out, autoreset_mode="same_step"):
     """(obs, rewards, terminations, truncations, infos) from host copies of the outputs: one
-    fs_host_convert pass over all rows, and one over the terminated arenas' final records."""
+    fs_host_convert pass over all rows -- running on the library's threads while this thread
+    builds the terminated arenas' final-observation dicts (fs_host_convert_start / _wait) -- and one
+    over the terminated arenas' final records."""
     n = len(out["frame"])
-    obs, info, (rewards, term, trunc) = _host_convert(out, "", None, n, True)
+    obs, info, (rewards, term, trunc), hold = _host_convert_on(out, "", None, n, True, start=True)
+    try:
+        _final_entries(out, info, autoreset_mode)
+    finally:
+        check(lib().fs_host_convert_wait())
+        del hold
+    return obs, rewards, term, trunc, info
+
+
+def _final_entries(out, info, autoreset_mode):
+    """info's final_observation / final_info entries (gymnasium 0.29) of the arenas the step ended,
+    from the source outputs (the step's converted arrays may still be in conversion)."""
+    term = np.asarray(out["terminated"]) != 0
     if autoreset_mode == "same_step" and term.any():
         idx = np.nonzero(term)[0]
         # only the terminated arenas' final outputs are converted
@@ -226,7 +247,6 @@ def step_result_from_outputs(out, autoreset_mode="same_step"):
         info["_final_observation"] = term.copy()
         info["final_info"] = final_info
         info["_final_info"] = term.copy()
-    return obs, rewards, term, trunc, info
 
 
 class FootsiesVectorEnv(_VectorEnvBase):

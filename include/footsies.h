@@ -422,6 +422,16 @@ typedef struct fs_host_arrays {
  * without rows, n > n_src.  (ABI 5 added n_src.) */
 int fs_host_convert(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n, const fs_host_arrays* dst,
                     int threads);
+/* fs_host_convert started on the library's own threads, returning once its arguments are checked
+ * (the same checks and errors); fs_host_convert_wait returns when it has finished.  The caller
+ * goes on meanwhile -- FootsiesVectorEnv.step builds the terminated arenas' final-observation
+ * dicts (Python, holding the GIL) while the step's arrays are converted -- and keeps src, rows and
+ * dst valid until the wait.  One conversion in flight per process: a start while another (another
+ * thread's) is in flight waits for it first; a wait returns once none is in flight.  fs_host_convert
+ * calls for fewer than 8192 rows run on the calling thread and may overlap it.  (ABI 6.) */
+int fs_host_convert_start(const fs_outputs* src, int64_t n_src, const int64_t* rows, int64_t n,
+                          const fs_host_arrays* dst, int threads);
+int fs_host_convert_wait(void);
 
 /* Pack the current outputs into one FS_RECORD_BYTES record per arena at dst (device,
  * [N][40] bytes): guard[2] move[2] action[2] hitstun[2] u8, terminated u8, truncated

@@ -423,3 +423,70 @@ def test_native_host_conversion_rejects_rows_outside_the_source():
         assert L.fs_host_convert(C.byref(so), n_src, r.ctypes.data, len(r), C.byref(dst), 1) == _abi.FS_E_INVALID
     assert L.fs_host_convert(C.byref(so), n_src, None, n_src + 1, C.byref(dst), 1) == _abi.FS_E_INVALID
     assert L.fs_host_convert(C.byref(so), n_src, None, n_src, C.byref(dst), 1) == _abi.FS_OK
+
+
+def test_native_host_conversion_started_and_waited():
+    """fs_host_convert_start / _wait (FootsiesVectorEnv.step's main conversion, overlapped with its
+    final-observation dicts): the same arrays as fs_host_convert over 100 000 rows (several pool
+    threads), the same argument checks at the start, a wait with nothing in flight returns, and a
+    start while one is in flight (another thread's) waits for it; step_result_from_outputs with it
+    equals the synchronous conversion."""
+    import ctypes as C
+    import threading
+    from footsies_gym_amd import _abi
+    from footsies_gym_amd._lib import lib
+    from footsies_gym_amd.vector_env import _host_convert
+    rng = np.random.default_rng(5)
+    n = 100_000
+    src = {"guard": rng.integers(0, 4, (n, 2)).astype(np.uint8), "move": rng.integers(0, 17, (n, 2)).astype(np.uint8),
+           "move_frame": rng.random((n, 2), np.float32), "position": rng.random((n, 2), np.float32),
+           "action": rng.integers(0, 8, (n, 2)).astype(np.uint8), "hitstun": rng.integers(0, 30, (n, 2)).astype(np.uint8),
+           "frame": rng.integers(0, 9999, n).astype(np.int32), "reward": rng.standard_normal(n),
+           "terminated": (rng.random(n) < 0.01).astype(np.uint8), "truncated": np.zeros(n, np.uint8)}
+    so = _abi.fs_outputs(**{k: v.ctypes.data for k, v in src.items()})
+    L = lib()
+    outs = []
+    for start in (False, True):
+        g = np.zeros((n, 2), np.int64)
+        mf = np.zeros((n, 2), np.float32)
+        fr = np.zeros(n, np.int64)
+        a1 = np.zeros((n, 3), np.uint8)
+        dst = _abi.fs_host_arrays(guard=g.ctypes.data, move_frame=mf.ctypes.data, frame=fr.ctypes.data,
+                                  p1_action=a1.ctypes.data)
+        if start:
+            assert L.fs_host_convert_start(C.byref(so), n, None, n, C.byref(dst), 4) == _abi.FS_OK
+            assert L.fs_host_convert_wait() == _abi.FS_OK
+        else:
+            assert L.fs_host_convert(C.byref(so), n, None, n, C.byref(dst), 4) == _abi.FS_OK
+        outs.append((g, mf, fr, a1))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    assert L.fs_host_convert_wait() == _abi.FS_OK  # nothing in flight
+    bad = np.array([n], np.int64)
+    assert L.fs_host_convert_start(C.byref(so), n, bad.ctypes.data, 1, C.byref(dst), 4) == _abi.FS_E_INVALID
+    # two threads: each start waits for the other's conversion, each wait for its own
+    res = []
+
+    def convert():
+        d = np.zeros((n, 2), np.int64)
+        hd = _abi.fs_host_arrays(guard=d.ctypes.data)
+        rc = L.fs_host_convert_start(C.byref(so), n, None, n, C.byref(hd), 2)
+        rc |= L.fs_host_convert_wait()
+        res.append((rc, np.array_equal(d, src["guard"])))
+    ts = [threading.Thread(target=convert) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert res == [(0, True)] * 4
+    # the VectorEnv step path (started conversion + final dicts) against the synchronous one
+    out = {k: v for k, v in src.items()}
+    out.update({"final_" + k: src[k] for k in ("guard", "move", "move_frame", "position", "frame", "action", "hitstun")})
+    obs, rew, term, trunc, info = step_result_from_outputs(out, "same_step")
+    obs2, info2, (rew2, term2, trunc2) = _host_convert(out, "", None, n, True)
+    for k in obs:
+        assert np.array_equal(obs[k], obs2[k]), k
+    assert np.array_equal(rew, rew2) and np.array_equal(term, term2) and np.array_equal(trunc, trunc2)
+    idx = np.nonzero(src["terminated"])[0]
+    assert len(idx) > 0 and np.array_equal(info["_final_observation"], src["terminated"] != 0)
+    assert all(info["final_observation"][i]["guard"].tolist() == src["guard"][i].tolist() for i in idx)
