@@ -122,3 +122,22 @@ def test_one_hip_runtime_per_process():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.split()[-2:] == ["1", "1"], r.stdout
+
+
+def test_ppo_grad_runs_argument_checks():
+    """fs_ppo_grad_runs rejects on the host, before any launch: no runs, n_runs <= 0, a run shift
+    outside [0, 30], a table shorter than one run (no GPU needed: nothing is launched)."""
+    from footsies_gym_amd._lib import lib as load
+    L = load()
+    rows = (C.c_float * 48)()
+    runs = (C.c_int64 * 4)()
+    mlp = _abi.fs_mlp()
+    ws = (C.c_uint8 * 16)()
+
+    def call(runs_ptr, n_rows, n_runs, shift):
+        return L.fs_ppo_grad_runs(C.cast(rows, C.c_void_p), n_rows, runs_ptr, n_runs, shift, C.byref(mlp),
+                                  C.byref(mlp), 0.2, 0.5, 0.01, C.cast(rows, C.c_void_p), C.cast(rows, C.c_void_p),
+                                  C.cast(ws, C.c_void_p), 16, None, _abi.FS_PPO_SPLIT_BF16)
+    rp = C.cast(runs, C.c_void_p)
+    for args in ((None, 4, 4, 0), (rp, 4, 0, 0), (rp, 4, 4, -1), (rp, 4, 4, 31), (rp, 4, 4, 3), (rp, 0, 4, 0)):
+        assert call(*args) == _abi.FS_E_INVALID, args
