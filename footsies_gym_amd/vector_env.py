@@ -223,8 +223,10 @@ def step_result_from_outputs(out, autoreset_mode="same_step"):
 def _final_entries(out, info, autoreset_mode):
     """info's final_observation / final_info entries (gymnasium 0.29) of the arenas the step ended,
     from the source outputs (the step's converted arrays may still be in conversion)."""
+    if autoreset_mode != "same_step":
+        return
     term = np.asarray(out["terminated"]) != 0
-    if autoreset_mode == "same_step" and term.any():
+    if term.any():
         idx = np.nonzero(term)[0]
         # only the terminated arenas' final outputs are converted
         fobs, finfo, _ = _host_convert(out, "final_", idx, len(idx), False, info_copies=False)
