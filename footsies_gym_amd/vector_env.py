@@ -211,6 +211,10 @@ def step_result_from_outputs(out, autoreset_mode="same_step"):
     builds the terminated arenas' final-observation dicts (fs_host_convert_start / _wait) -- and one
     over the terminated arenas' final records."""
     n = len(out["frame"])
+    if n < _ASYNC_MIN_ROWS:  # (fs_host_convert runs these on the calling thread anyway)
+        obs, info, (rewards, term, trunc) = _host_convert(out, "", None, n, True)
+        _final_entries(out, info, autoreset_mode)
+        return obs, rewards, term, trunc, info
     obs, info, (rewards, term, trunc), hold = _host_convert_on(out, "", None, n, True, start=True)
     try:
         _final_entries(out, info, autoreset_mode)
@@ -218,6 +222,11 @@ def step_result_from_outputs(out, autoreset_mode="same_step"):
         check(lib().fs_host_convert_wait())
         del hold
     return obs, rewards, term, trunc, info
+
+
+# below this many rows fs_host_convert converts on the calling thread (fs_api.cpp host_convert_run),
+# and handing the conversion to the library's runner thread would only add its wake-up
+_ASYNC_MIN_ROWS = 8192
 
 
 def _final_entries(out, info, autoreset_mode):
