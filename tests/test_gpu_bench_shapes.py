@@ -124,3 +124,34 @@ def run_shape(oracle_lib, actors, shape, n):
     assert out["terminated"].any()  # rounds end inside the compared launches (final records ran)
     sim.close()
     ora.close()
+
+
+@pytest.mark.parametrize("actors", ["external", "bot"])
+def test_headline_kernel_long_horizon(oracle_lib, actors):
+    """The headline kernel over SURVEY 8(d)'s C3 horizon many times over: 20 consecutive
+    1000-tick launches (20 000 ticks: hundreds of rounds per arena, KOs, auto-resets, bot plans)
+    at 65 536 arenas over HBM rows from fs_hash_actions, the arenas' state carried in HBM; the
+    oracle steps the same rows tick by tick (OpenMP on the host).  Every record of the last launch
+    and the full canonical state at the end must be equal."""
+    import torch
+    from footsies_gym_amd.simulator import unpack_trajectory
+    launches, T = 20, 1000
+    sim, ora = _pair(oracle_lib, actors, N)
+    ext = actors != "bot"
+    traj = sim.alloc_packed_trajectory(T)
+    for j in range(launches):
+        p1, p2 = sim.hash_actions(T, seed=SEED, t0=j * T, p2=ext)
+        sim.step_n_packed(T, p1, p2 if ext else None, trajectory=traj)
+        torch.cuda.synchronize()
+        h1 = p1.cpu().numpy()
+        h2 = p2.cpu().numpy() if ext else None
+        last = j == launches - 1
+        for t in range(T):
+            exp = ora.step(h1[t], h2[t] if ext else None)
+            if last and t % 97 in (0, 96):  # (a sample of the last launch's records, unpacked on the host)
+                rec = {key: (None if v is None else v[t].cpu().numpy()) for key, v in traj.items()}
+                compare_outputs(exp, {key: np.ascontiguousarray(v) for key, v in unpack_trajectory(rec).items()},
+                                step=j * T + t)
+    compare_states(ora.state(), sim.get_state(), step=launches * T)
+    sim.close()
+    ora.close()
