@@ -126,17 +126,20 @@ def run_shape(oracle_lib, actors, shape, n):
     ora.close()
 
 
-@pytest.mark.parametrize("actors", ["external", "bot"])
-def test_headline_kernel_long_horizon(oracle_lib, actors):
+@pytest.mark.parametrize("actors,n", [("external", N), ("bot", N), ("external", 32768)])
+def test_headline_kernel_long_horizon(oracle_lib, actors, n):
     """The headline kernel over SURVEY 8(d)'s C3 horizon many times over: 20 consecutive
     1000-tick launches (20 000 ticks: hundreds of rounds per arena, KOs, auto-resets, bot plans)
     at 65 536 arenas over HBM rows from fs_hash_actions, the arenas' state carried in HBM; the
     oracle steps the same rows tick by tick (OpenMP on the host).  Every record of the last launch
-    and the full canonical state at the end must be equal."""
+    and the full canonical state at the end must be equal.  Also at C4's per-GPU 32 768 arenas,
+    where the request-prefetch kernel runs."""
     import torch
+    from footsies_gym_amd._lib import lib
     from footsies_gym_amd.simulator import unpack_trajectory
     launches, T = 20, 1000
-    sim, ora = _pair(oracle_lib, actors, N)
+    sim, ora = _pair(oracle_lib, actors, n)
+    assert lib().fs_step_kernel(sim.handle, T, _abi.FS_KERNEL_PACKED).decode() == fused_kernel(KERNEL[actors], n)
     ext = actors != "bot"
     traj = sim.alloc_packed_trajectory(T)
     for j in range(launches):
