@@ -12,6 +12,8 @@ leg after the other, each preceded by a marker dispatch (torch.cuda._sleep, rocp
 `spin_kernel`): the reduction assigns every k_step dispatch to the leg whose marker precedes it and
 reports per leg the dispatch count and the average / median / min / max / p99 duration, plus the
 launch-to-launch period (start of one dispatch to the start of the next, within the leg).
+The `venv_torch_policy` leg produces each step's actions on the device just before the step (a
+policy's sampling), where the other legs read rows written long before (from HBM).
 """
 import argparse
 import ctypes as C
@@ -24,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 # in marker order; the "warm_*" sections (warm-ups between the timed legs) are traced but not reported
 LEGS = ["step", "step_warm_first", "host_actions", "step_gather", "warm_venv_torch", "venv_torch", "warm_venv_numpy",
-        "venv_numpy", "warm_single_env", "single_env"]
+        "venv_numpy", "warm_venv_policy", "venv_torch_policy", "warm_single_env", "single_env"]
 
 
 def run(n, steps):
@@ -102,6 +104,20 @@ def run(n, steps):
             env.step(acts[j])
         torch.cuda.synchronize()
         env.close()
+    # "venv_torch_policy": the torch VectorEnv with each step's actions produced on the device just
+    # before the step, as a policy's sampling would (the rows are then fresh in L2, not read from HBM)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    opp = [None]
+    env = FootsiesVectorEnv(n, opponent=lambda o, i: opp[0], output="torch", seed=0)
+    env.reset(seed=0)
+    for leg_steps in (400, 200):  # the warm-up section, then the reported one
+        marker()
+        for j in range(leg_steps):
+            a = torch.randint(0, 8, (n,), generator=g, device="cuda", dtype=torch.uint8)
+            opp[0] = torch.randint(0, 8, (n,), generator=g, device="cuda", dtype=torch.uint8)
+            env.step(a)
+    torch.cuda.synchronize()
+    env.close()
     # "single_env": the one-arena FootsiesEnv vs the bot
     env = FootsiesEnv(seed=0)
     env.reset(seed=0)
