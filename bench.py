@@ -666,17 +666,18 @@ def main():
             if rc:
                 check(rc, h)
     host_rate = N * kh / leg_median(run_host, 0, kh)
-    # the per-step path with the multi-GPU exchange of SURVEY 8(e): every step's outputs packed
-    # on device into 40-B records (fs_pack_outputs) and gathered over RCCL/xGMI
+    # the per-step path with the multi-GPU exchange of SURVEY 8(e): every step's outputs written
+    # as 40-B records by the step kernel itself (fs_step_rec; before r05: fs_step + a separate
+    # fs_pack_outputs launch) and gathered over RCCL/xGMI
     kg = min(K, 500)
     rec = torch.empty((N, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=dev)
     gbuf = torch.empty((world * N, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=dev)
-    fs_pack = L.fs_pack_outputs
+    fs_step_rec = L.fs_step_rec
+    recp = C.c_void_p(rec.data_ptr())
 
     def run_step_gather(k0, n):
         for k in range(k0, k0 + n):
-            rc = fs_step(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE)
-            rc = rc or fs_pack(h, C.c_void_p(rec.data_ptr()))
+            rc = fs_step_rec(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE, recp)
             if rc:
                 check(rc, h)
             if grouped and args.dist_backend == "nccl":
@@ -686,8 +687,7 @@ def main():
     def run_step_gather_root(k0, n):  # the learner-only variant: grouped send / recv to rank 0
         from footsies_gym_amd.parallel import gather_records_to
         for k in range(k0, k0 + n):
-            rc = fs_step(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE)
-            rc = rc or fs_pack(h, C.c_void_p(rec.data_ptr()))
+            rc = fs_step_rec(h, C.c_void_p(base1 + k * N), C.c_void_p(base2 + k * N), _abi.FS_ACT_DEVICE, recp)
             if rc:
                 check(rc, h)
             if grouped and args.dist_backend == "nccl":
@@ -783,12 +783,12 @@ def main():
                                            "the gather legs: one untimed call, then the median of `regions` regions"},
         "step_gather_mode": {"value": world * N * kg / gwall, "ms_per_step": 1e3 * gwall / kg, "steps": kg,
                              "bytes_gathered_per_step": world * N * _abi.FS_RECORD_BYTES,
-                             "note": "fs_step + fs_pack_outputs + one all_gather_into_tensor of the 40-B "
+                             "note": "fs_step_rec (records from the step kernel) + one all_gather_into_tensor of the 40-B "
                                      "(obs, reward, done) records over RCCL per step (none without a process group -- a plain "
                                      "1-GPU run -- or with --dist-backend gloo)"},
         "step_gather_root_mode": {"value": world * N * kg / grwall, "ms_per_step": 1e3 * grwall / kg, "steps": kg,
                                   "bytes_into_rank0_per_step": (world - 1) * N * _abi.FS_RECORD_BYTES,
-                                  "note": "fs_step + fs_pack_outputs + the records of every rank gathered to rank 0 "
+                                  "note": "fs_step_rec + the records of every rank gathered to rank 0 "
                                           "only (grouped send / recv over RCCL, parallel.gather_records_to)"},
     }
     # the fused legs beside the headline, on every rank (barrier + max over ranks, like the

@@ -183,6 +183,7 @@ LIB_FUNCTIONS = {
     "fs_hash_actions": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "fs_outputs_get": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_pack_outputs": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "fs_step_rec": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "fs_bind_outputs": (C.c_int, [C.c_void_p, C.POINTER(fs_outputs)]),
     "fs_get_env_state": (C.c_int, [C.c_void_p, C.POINTER(fs_env_state)]),
     "fs_get_state": (C.c_int, [C.c_void_p, C.POINTER(fs_arena_state)]),

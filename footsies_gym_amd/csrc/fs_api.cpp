@@ -312,7 +312,7 @@ FS_API int fs_reset(fs_handle h, const uint64_t* seeds, const uint8_t* mask, int
 
 static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2, int flags, uint64_t seed,
                        const fs_outputs* traj, const uint8_t* active = nullptr,
-                       const fs_policy* pol = nullptr, const fs_packed_traj* pk = nullptr) {
+                       const fs_policy* pol = nullptr, const fs_packed_traj* pk = nullptr, void* rec = nullptr) {
   int rc;
   if ((rc = use_device(h))) return rc;
   const size_t N = (size_t)h->n;
@@ -331,6 +331,7 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
   sp.p2_resets = h->cfg.p2_mode == FS_P2_BOT;
   sp.p2_noop = h->cfg.p2_mode == FS_P2_NOOP;
   sp.geom = h->geom;
+  sp.rec = static_cast<uint2*>(rec);  // (one-tick launches only: fs_step_rec)
   if (pol) sp.pol = fsk::PolicyParams{pol->w1, pol->b1, pol->w2, pol->b2, pol->w3, pol->b3,
                                       pol->actions_out, pol->logp_out, pol->seed};
   const bool ext = h->cfg.p2_mode == FS_P2_EXTERNAL;
@@ -362,9 +363,9 @@ static int step_common(fs_handle h, int n, const uint8_t* p1, const uint8_t* p2,
     sp.p2 = ext ? h->d_act + N : nullptr;
     sp.active = active ? h->d_mask : nullptr;
   } else {
-    // P1 bot with explicit P2 rows: P1's row is never read, but a null p1 would select the
-    // hashed-action kernel, so it points at the staging row
-    sp.p1 = (p1_bot && !p1 && p2) ? h->d_act : p1;
+    // P1 bot with explicit P2 rows (or records to write, which only k_step does): P1's row is
+    // never read, but a null p1 would select the hashed-action kernel, so it points at the staging row
+    sp.p1 = (p1_bot && !p1 && (p2 || rec)) ? h->d_act : p1;
     sp.p2 = ext ? p2 : nullptr;
     sp.active = active;
   }
@@ -487,6 +488,21 @@ FS_API int fs_step(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, in
     return set_err(h, FS_E_INVALID, "fs_step: p2 actions required for FS_P2_EXTERNAL");
   if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
   return step_common(h, 1, p1_act, p2_act, flags, 0, nullptr);
+}
+
+FS_API int fs_step_rec(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags, void* rec) {
+  if (!h) return FS_E_INVALID;
+  if (!rec) return set_err(h, FS_E_INVALID, "fs_step_rec: record destination required");
+  if (reinterpret_cast<uintptr_t>(rec) % 8) return set_err(h, FS_E_INVALID, "fs_step_rec: records must be 8-byte aligned");
+  if (h->cfg.frame_delay > 0) {  // (the delayed queue rewrites the outputs after the tick: pack those)
+    const int rc = fs_step(h, p1_act, p2_act, flags);
+    return rc ? rc : fs_pack_outputs(h, rec);
+  }
+  if (!p1_act && h->cfg.p1_mode != FS_P1_BOT) return set_err(h, FS_E_INVALID, "fs_step_rec: p1 actions required");
+  if (h->cfg.p2_mode == FS_P2_EXTERNAL && !p2_act)
+    return set_err(h, FS_E_INVALID, "fs_step_rec: p2 actions required for FS_P2_EXTERNAL");
+  if (flags != FS_ACT_HOST && flags != FS_ACT_DEVICE) return set_err(h, FS_E_INVALID, "bad flags %d", flags);
+  return step_common(h, 1, p1_act, p2_act, flags, 0, nullptr, nullptr, nullptr, nullptr, rec);
 }
 
 FS_API int fs_step_masked(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, const uint8_t* active,

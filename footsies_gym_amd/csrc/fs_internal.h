@@ -93,6 +93,7 @@ struct StepParams {
   int prio;       // fused launches: time-sliced wave priority (set by the launcher, prio_slice)
   int geom;       // some arena has position.y != 0 or a flipped facing: the general-geometry tick
   int prefetch;   // two-lane fused row launches: each tick's request prepared at the end of the tick before
+  uint2* rec;     // one-tick launches (fs_step_rec): each arena's FS_RECORD_BYTES record, or null
   // host actions of a one-tick launch over at most kInlineArenas arenas, carried in the kernel
   // arguments instead of a staging copy (inl_n != 0): byte a of inl[player] is arena a's input
   int inl_n;

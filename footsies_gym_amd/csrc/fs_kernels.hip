@@ -1319,6 +1319,26 @@ __device__ __forceinline__ void write_packed(const Lane& L, uint4* base, uint32_
   st_off(reinterpret_cast<PkRec*>(base), 16u * (2u * r + L.k), packed_record(L, w3));
 }
 
+// fs_step_rec: arena r's FS_RECORD_BYTES gather record (fs_gather.hip k_pack_records' layout:
+// guard[2] move[2] action[2] hitstun[2] terminated truncated pad[2] move_frame[2] position[2] frame
+// reward) from the values write_obs stores, written by lane 0 after one pair exchange.  Both lanes
+// must call it (the exchange reads the partner's registers).
+__device__ __forceinline__ void write_record(const Lane& L, uint2* rec, uint32_t r, uint32_t terminated,
+                                             double reward) {
+  const PkRec v = packed_record(L, 0u);  // bytes guard | move | action | hitstun, move_frame, position
+  const uint32_t ox = xpair(v.x), oy = xpair(v.y), oz = xpair(v.z);
+  if (L.k == 0) {
+    uint2* d = rec + 5u * r;
+    // (bytes b0..b3 of P1's word, b4..b7 of P2's: guard0 guard1 move0 move1 | action0 action1 hitstun0 hitstun1)
+    d[0] = make_uint2(__builtin_amdgcn_perm(ox, v.x, 0x05010400u), __builtin_amdgcn_perm(ox, v.x, 0x07030602u));
+    d[1] = make_uint2(terminated, v.y);  // (truncated and the pad bytes: 0)
+    d[2] = make_uint2(oy, v.z);
+    d[3] = make_uint2(oz, (uint32_t)L.frame_count);
+    const uint64_t rw = (uint64_t)__double_as_longlong(reward);
+    d[4] = make_uint2((uint32_t)rw, (uint32_t)(rw >> 32));
+  }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1462,6 +1482,9 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
       st_off(o.reward, 8 * r, 0.0);  // per-arena outputs: both lanes store the same value (no divergent branch)
       st_off(o.terminated, r, (uint8_t)0);
       st_off(o.truncated, r, (uint8_t)0);
+      if constexpr (G) {
+        if (p.rec) write_record(L, p.rec, r, 0u, 0.0);
+      }
     }
     opaque_burst_results(L);
     return;
@@ -1607,6 +1630,9 @@ __device__ __forceinline__ void env_step(Lane& L, uint32_t a_own, const StepPara
     st_off(o.reward, 8 * r, reward);  // identical on both lanes of the arena
     st_off(o.terminated, r, (uint8_t)(over ? 1 : 0));
     st_off(o.truncated, r, (uint8_t)0);
+    if constexpr (G) {
+      if (p.rec) write_record(L, p.rec, r, over ? 1u : 0u, reward);
+    }
   }
   // all four words live until here (the tick reads three; see R.push above)
   if constexpr (!G) asm volatile("" ::"v"(L.ai));

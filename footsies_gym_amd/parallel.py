@@ -146,6 +146,16 @@ class ShardedSim:
         g = gather_records_to(rec, dst, group, self.sizes)
         return None if g is None else unpack_outputs(g, torch)
 
+    def step_gather(self, p1, p2=None, group=None, dst=None):
+        """step() and gather() in one: the step's kernel writes the records (fs_step_rec) that
+        gather() would pack, then the same all_gather (dst=None) or send / recv to rank dst."""
+        import torch
+        rec = self.sim.step_records(p1, p2)
+        if dst is None:
+            return unpack_outputs(gather_records(rec, group, self.sizes), torch)
+        g = gather_records_to(rec, dst, group, self.sizes)
+        return None if g is None else unpack_outputs(g, torch)
+
     def close(self):
         self.sim.close()
 

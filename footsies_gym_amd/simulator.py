@@ -298,6 +298,25 @@ class FootsiesSim:
             check(lib().fs_sync(self._h), self._h)
         return self._out
 
+    def step_records(self, p1, p2=None, dst=None):
+        """step() of every arena that also writes the step's 40-byte records (fs_step_rec: the
+        bytes pack_outputs would, from the tick's own kernel); device uint8 [N] actions (p1 may
+        be None with p1_mode="bot").  Returns the [N, 40] uint8 device records."""
+        torch = _torch()
+        if dst is None:
+            dst = torch.empty((self.num_envs, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=self.device)
+        self._check_device(dst, "dst", torch.uint8, self.num_envs * _abi.FS_RECORD_BYTES)
+        ext = self.p2_mode == "external"
+        q1 = None if p1 is None else _as_u8_device(_to_device(p1, self.device), self.num_envs)
+        q2 = _as_u8_device(_to_device(p2, self.device), self.num_envs) if ext else None
+        if q1 is None and self.p1_mode != "bot":
+            raise ValueError("p1 actions are required unless p1_mode='bot'")
+        check(lib().fs_step_rec(self._h, None if q1 is None else C.c_void_p(q1.data_ptr()),
+                                None if q2 is None else C.c_void_p(q2.data_ptr()), _abi.FS_ACT_DEVICE,
+                                C.c_void_p(dst.data_ptr())), self._h)
+        self._ready_out()
+        return dst
+
     def pack_outputs(self, dst=None):
         """The current outputs as one 40-byte record per arena ([N, 40] uint8 device tensor,
         parallel.RECORD_BYTES layout) by one kernel (fs_pack_outputs): the gather payload."""

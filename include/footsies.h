@@ -439,6 +439,12 @@ int fs_host_convert_wait(void);
  * of the multi-GPU per-step gather over RCCL.  Asynchronous. */
 #define FS_RECORD_BYTES 40
 int fs_pack_outputs(fs_handle h, void* dst);
+/* fs_step that also writes every arena's FS_RECORD_BYTES record (fs_pack_outputs' layout) to rec
+ * (device, [N][40] bytes, 8-byte aligned) from inside the tick's own kernel: the same bytes as
+ * fs_step followed by fs_pack_outputs(h, rec), one launch instead of two -- the per-step gather
+ * path of SURVEY.md 8(e).  With frame_delay > 0 (the delayed queue rewrites the outputs after the
+ * tick) it is exactly those two calls.  Asynchronous.  (ABI 6.) */
+int fs_step_rec(fs_handle h, const uint8_t* p1_act, const uint8_t* p2_act, int flags, void* rec);
 
 /* Redirect the per-step outputs into caller-owned device buffers (e.g. torch
  * tensors) for zero-copy; NULL members keep the library's own buffer.  The

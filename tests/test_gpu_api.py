@@ -471,6 +471,75 @@ def test_pack_outputs_kernel_matches_host_packing():
         assert bool(torch.equal(v, sim.outputs()[k])), k
 
 
+@pytest.mark.parametrize("n,kw", [
+    (1003, dict(p2_mode="external")),
+    (1003, dict(p2_mode="bot", dense_reward=False)),
+    (1003, dict(p2_mode="external", autoreset_mode="next_step", float_mode="double")),
+    (777, dict(p2_mode="bot", p1_mode="bot", autoreset_mode="next_step")),
+    (3, dict(p2_mode="external")),  # few arenas: host actions travel in the kernel arguments
+    (513, dict(p2_mode="external", frame_delay=2)),  # the delayed queue: fs_step + fs_pack_outputs
+])
+def test_step_rec_equals_step_then_pack(n, kw):
+    """fs_step_rec (k_step writes the 40-byte gather records itself) == fs_step followed by
+    fs_pack_outputs, byte for byte, on twin handles over 400 steps with terminal and reset rows,
+    and the outputs the handle keeps are the same as well."""
+    import torch
+    from footsies_gym_amd import parallel
+    from footsies_gym_amd.simulator import FootsiesSim
+    a, b = FootsiesSim(n, seed=4, **kw), FootsiesSim(n, seed=4, **kw)
+    p1, p2 = a.hash_actions(400, seed=13)
+    host = n <= 8
+    terminals = 0
+    for t in range(400):
+        q1 = None if kw.get("p1_mode") == "bot" else p1[t]
+        q2 = p2[t] if kw["p2_mode"] == "external" else None
+        if host:
+            b.step(q1.cpu().numpy(), q2.cpu().numpy())
+        else:
+            b.step(q1 if q1 is not None else None, q2)
+        want = b.pack_outputs()
+        got = a.step_records(q1, q2) if not host else _step_rec_host(a, q1, q2)
+        assert bool(torch.equal(got, want)), (t, (got != want).nonzero()[:4].tolist())
+        terminals += int(b.outputs()["terminated"].sum())
+    assert terminals > 0
+    for k, v in b.outputs().items():
+        assert bool(torch.equal(v, a.outputs()[k])), k
+    back = parallel.unpack_outputs(got, torch)
+    for k, v in back.items():
+        assert bool(torch.equal(v, b.outputs()[k])), k
+
+
+def _step_rec_host(sim, q1, q2):
+    """fs_step_rec with host action bytes (the few-arena inline-argument path)."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    from footsies_gym_amd import _abi
+    from footsies_gym_amd._lib import check, lib
+    a1 = np.ascontiguousarray(q1.cpu().numpy())
+    a2 = np.ascontiguousarray(q2.cpu().numpy())
+    dst = torch.empty((sim.num_envs, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=sim.device)
+    check(lib().fs_step_rec(sim._h, a1.ctypes.data, a2.ctypes.data, _abi.FS_ACT_HOST, C.c_void_p(dst.data_ptr())),
+          sim._h)
+    return dst
+
+
+def test_step_rec_rejects_bad_destinations():
+    import ctypes as C
+    from footsies_gym_amd import _abi
+    from footsies_gym_amd._lib import lib
+    from footsies_gym_amd.simulator import FootsiesSim
+    import torch
+    s = FootsiesSim(16, p2_mode="bot")
+    a = torch.zeros(16, dtype=torch.uint8, device=s.device)
+    buf = torch.zeros(16 * 40 + 8, dtype=torch.uint8, device=s.device)
+    assert lib().fs_step_rec(s._h, C.c_void_p(a.data_ptr()), None, _abi.FS_ACT_DEVICE, None) == _abi.FS_E_INVALID
+    assert lib().fs_step_rec(s._h, C.c_void_p(a.data_ptr()), None, _abi.FS_ACT_DEVICE,
+                             C.c_void_p(buf.data_ptr() + 4)) == _abi.FS_E_INVALID
+    with pytest.raises(ValueError):
+        s.step_records(a, dst=buf[:100])
+
+
 @pytest.mark.parametrize("extra", [[], ["--global-envs", "4096", "--mode", "step"]])
 def test_bench_json_contract(extra):
     """bench.py prints one JSON line with the driver's fields, the roofline and (1 GPU) the

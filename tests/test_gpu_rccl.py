@@ -55,8 +55,15 @@ def _worker(port, q):
     every = {k: v.cpu().numpy() for k, v in sim.gather().items()}
     root = {k: v.cpu().numpy() for k, v in sim.gather(dst=0).items()}
     local = {k: v.cpu().numpy() for k, v in unpack_outputs(sim.sim.pack_outputs(), torch).items()}
+    # step_gather: the step kernel writes the records (fs_step_rec), then the same collectives
+    a1 = torch.full((777,), 3, dtype=torch.uint8, device="cuda:0")
+    sg = {k: v.cpu().numpy() for k, v in sim.step_gather(a1).items()}
+    sg_local = {k: v.cpu().numpy() for k, v in unpack_outputs(sim.sim.pack_outputs(), torch).items()}
+    sg_root = {k: v.cpu().numpy() for k, v in sim.step_gather(a1, dst=0).items()}
+    sg_local2 = {k: v.cpu().numpy() for k, v in unpack_outputs(sim.sim.pack_outputs(), torch).items()}
     dist.barrier()
-    q.put({"backend": dist.get_backend(), "every": every, "root": root, "local": local})
+    q.put({"backend": dist.get_backend(), "every": every, "root": root, "local": local,
+           "sg": (sg, sg_local), "sg_root": (sg_root, sg_local2)})
     sim.close()
     dist.destroy_process_group()
 
@@ -75,3 +82,6 @@ def test_sharded_gather_over_rccl_world_one():
         assert r["every"][k].tobytes() == v.tobytes(), k
         assert r["root"][k].tobytes() == v.tobytes(), k
     assert np.any(r["local"]["frame"] != 0)
+    for got, want in (r["sg"], r["sg_root"]):
+        for k, v in want.items():
+            assert got[k].tobytes() == v.tobytes(), k
