@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 # in marker order; the "warm_*" sections (warm-ups between the timed legs) are traced but not reported
-LEGS = ["step", "step_warm_first", "host_actions", "step_gather", "warm_venv_torch", "venv_torch", "warm_venv_numpy",
+LEGS = ["step", "step_warm_first", "host_actions", "step_gather", "step_rec", "warm_venv_torch", "venv_torch", "warm_venv_numpy",
         "venv_numpy", "warm_venv_policy", "venv_torch_policy", "warm_single_env", "single_env"]
 
 
@@ -77,6 +77,11 @@ def run(n, steps):
     for k in range(500):
         step(k)
         check(L.fs_pack_outputs(h, C.c_void_p(rec.data_ptr())), h)
+    # "step_rec": fs_step_rec (the same records from k_step itself: one launch per step)
+    marker()
+    recp = C.c_void_p(rec.data_ptr())
+    for k in range(500):
+        check(L.fs_step_rec(h, C.c_void_p(b1 + k * n), C.c_void_p(b2 + k * n), _abi.FS_ACT_DEVICE, recp), h)
     torch.cuda.synchronize()
     sim.close()
     # the VectorEnv legs (bench.py vector_env_rate): torch output, then numpy output (its kernels
