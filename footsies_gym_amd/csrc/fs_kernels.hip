@@ -1321,21 +1321,34 @@ __device__ __forceinline__ void write_packed(const Lane& L, uint4* base, uint32_
 
 // fs_step_rec: arena r's FS_RECORD_BYTES gather record (fs_gather.hip k_pack_records' layout:
 // guard[2] move[2] action[2] hitstun[2] terminated truncated pad[2] move_frame[2] position[2] frame
-// reward) from the values write_obs stores, written by lane 0 after one pair exchange.  Both lanes
-// must call it (the exchange reads the partner's registers).
+// reward) from the values write_obs stores.  Both lanes of the pair store 16 B in one instruction
+// -- lane 0 bytes 0-15 (the byte fields, the flags, P1's move_frame), lane 1 bytes 16-31 (P2's
+// move_frame, both positions, the frame) -- and lane 0 the f64 reward at byte 32: two stores per
+// wave instead of five, after two pair exchanges.  Both lanes must call it (the exchanges read the
+// partner's registers).  (The 16-B halves are 8-B aligned: 40 r + 16 k.)
+typedef uint32_t RecQ __attribute__((ext_vector_type(4), aligned(8)));
 __device__ __forceinline__ void write_record(const Lane& L, uint2* rec, uint32_t r, uint32_t terminated,
                                              double reward) {
   const PkRec v = packed_record(L, 0u);  // bytes guard | move | action | hitstun, move_frame, position
-  const uint32_t ox = xpair(v.x), oy = xpair(v.y), oz = xpair(v.z);
+  const uint32_t ox = xpair(v.x), oz = xpair(v.z);
+  RecQ q;
   if (L.k == 0) {
-    uint2* d = rec + 5u * r;
     // (bytes b0..b3 of P1's word, b4..b7 of P2's: guard0 guard1 move0 move1 | action0 action1 hitstun0 hitstun1)
-    d[0] = make_uint2(__builtin_amdgcn_perm(ox, v.x, 0x05010400u), __builtin_amdgcn_perm(ox, v.x, 0x07030602u));
-    d[1] = make_uint2(terminated, v.y);  // (truncated and the pad bytes: 0)
-    d[2] = make_uint2(oy, v.z);
-    d[3] = make_uint2(oz, (uint32_t)L.frame_count);
+    q.x = __builtin_amdgcn_perm(ox, v.x, 0x05010400u);
+    q.y = __builtin_amdgcn_perm(ox, v.x, 0x07030602u);
+    q.z = terminated;  // (truncated and the pad bytes: 0)
+    q.w = v.y;
+  } else {
+    q.x = v.y;
+    q.y = oz;
+    q.z = v.z;
+    q.w = (uint32_t)L.frame_count;
+  }
+  char* b = reinterpret_cast<char*>(rec) + 40u * r;
+  *reinterpret_cast<RecQ*>(b + 16u * L.k) = q;
+  if (L.k == 0) {
     const uint64_t rw = (uint64_t)__double_as_longlong(reward);
-    d[4] = make_uint2((uint32_t)rw, (uint32_t)(rw >> 32));
+    *reinterpret_cast<uint2*>(b + 32u) = make_uint2((uint32_t)rw, (uint32_t)(rw >> 32));
   }
 }
 
