@@ -158,3 +158,32 @@ def test_headline_kernel_long_horizon(oracle_lib, actors, n):
     compare_states(ora.state(), sim.get_state(), step=launches * T)
     sim.close()
     ora.close()
+
+
+def test_step_rec_gather_leg_matches_oracle(oracle_lib):
+    """bench.py's step_gather legs at their own shape: 65 536 arenas, `fs_step_rec` over HBM action
+    rows of the hashed stream, one call per step.  Every step's 40-B records, unpacked
+    (parallel.unpack_outputs), equal the oracle's outputs of that tick, and the state equals the
+    oracle's at the end."""
+    import ctypes as C
+    import torch
+    from footsies_gym_amd import parallel
+    from footsies_gym_amd._lib import check, lib
+    sim, ora = _pair(oracle_lib, "external")
+    T = 120
+    p1, p2 = sim.hash_actions(T, seed=SEED, t0=0)
+    torch.cuda.synchronize()
+    h1, h2 = p1.cpu().numpy(), p2.cpu().numpy()
+    rec = torch.empty((N, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=sim.device)
+    terminals = 0
+    for t in range(T):
+        check(lib().fs_step_rec(sim.handle, C.c_void_p(p1[t].data_ptr()), C.c_void_p(p2[t].data_ptr()),
+                                _abi.FS_ACT_DEVICE, C.c_void_p(rec.data_ptr())), sim.handle)
+        got = {k: v.cpu().numpy() for k, v in parallel.unpack_outputs(rec, torch).items()}
+        exp = ora.step(h1[t], h2[t])
+        compare_outputs(exp, got, step=t, same_step=False)
+        terminals += int(exp["terminated"].sum())
+    assert terminals > 0
+    compare_states(ora.state(), sim.get_state(), step=T)
+    sim.close()
+    ora.close()
