@@ -47,6 +47,17 @@ VENV_STEPS = 200        # timed FootsiesVectorEnv steps, after a warm-up into st
 
 
 LAYOUT_DEFAULT = "packed"
+C4_GLOBAL_ENVS = 262144  # BASELINE.json configs[3]: 262 144 arenas sharded over the node's GPUs
+
+
+def c4_split(world, rank, total=C4_GLOBAL_ENVS):
+    """The c4_strong leg's shard of this rank: (arenas, arena_base).  A contiguous range of the
+    global arena indices, so seeds and the hashed action rows (fs_config.arena_base) are those of
+    the same arenas in one unsharded run; 262 144 / N per rank (strong scaling)."""
+    if total % world:
+        return None  # (no even split: the leg is skipped and the line says why)
+    n = total // world
+    return n, rank * n
 
 
 def parse():
@@ -74,6 +85,8 @@ def parse():
     ap.add_argument("--roofline-ticks", type=int, default=1000,
                     help="ticks per fs_step_n launch of the roofline block (the shape profiles/ covers)")
     ap.add_argument("--no-extras", action="store_true", help="skip the C2 bot-opponent and C5 policy-loop rates")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the c4_strong leg (262 144 arenas split over the ranks, BASELINE configs[3])")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--dry-run", action="store_true",
@@ -435,8 +448,9 @@ def dry_run(args, world, rank):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         walls.append(float(t.item()))
     wall = sorted(walls)[len(walls) // 2]
-    mine = torch.tensor([float(N), sorted(local)[len(local) // 2]], dtype=torch.float64)
-    every = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+    c4n, c4b = c4_split(world, rank) or (0, -1)
+    mine = torch.tensor([float(N), sorted(local)[len(local) // 2], float(c4n), float(c4b)], dtype=torch.float64)
+    every = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
     if world > 1:
         dist.all_gather(every, mine)
     else:
@@ -449,7 +463,11 @@ def dry_run(args, world, rank):
                           "config": {"workload": "dry run", "envs_per_gpu": N, "global_envs": N * world,
                                      "parallelism": "arena-shard x%d" % world},
                           "ranks": {"world_size": world, "backend": dist.get_backend() if world > 1 else None,
-                                    "rank_walls_ms": [round(1e3 * float(e[1]), 4) for e in every]}}))
+                                    "rank_walls_ms": [round(1e3 * float(e[1]), 4) for e in every]},
+                          # the c4_strong leg's plan as every rank computed it (no simulator in a dry run)
+                          "c4_strong": {"global_envs": C4_GLOBAL_ENVS, "scaling": "strong",
+                                        "envs_per_rank": [int(e[2]) for e in every],
+                                        "arena_base_per_rank": [int(e[3]) for e in every]}}))
     if world > 1:
         dist.destroy_process_group()
 
@@ -490,7 +508,7 @@ def main():
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo reduces host tensors
 
     from footsies_gym_amd import _abi
-    from footsies_gym_amd._lib import check, lib
+    from footsies_gym_amd._lib import check, lib, library_info
     from footsies_gym_amd.simulator import FootsiesSim
 
     N, K, W = args.envs, args.steps, args.warmup
@@ -515,7 +533,9 @@ def main():
     fs_step, fs_step_n, fs_step_n_packed = L.fs_step, L.fs_step_n, L.fs_step_n_packed
     layout_flag = _abi.FS_KERNEL_PACKED if packed else 0
 
-    def make_runs(a1, a2, tr, ticks_per_launch, packed=packed):
+    def make_runs(a1, a2, tr, ticks_per_launch, packed=packed, handle=None, n=None):
+        h = handle if handle is not None else sim.handle
+        N = n if n is not None else sim.num_envs
         b1, b2 = a1.data_ptr(), a2.data_ptr()
         if packed:
             td = _abi.fs_packed_traj(lanes=tr["lanes"].data_ptr(), reward=tr["reward"].data_ptr(),
@@ -574,14 +594,15 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def rank_values(v):
-        """Every rank's value of v (this rank's median region wall), in rank order, in ms."""
+    def rank_values(v, raw=False):
+        """Every rank's value of v (this rank's median region wall), in rank order, in ms (raw: as given)."""
         t = torch.tensor([v], dtype=torch.float64, device=coll_dev)
         if world == 1:
-            return [round(1e3 * v, 4)]
-        every = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(every, t)
-        return [round(1e3 * float(e.item()), 4) for e in every]
+            every = [t]
+        else:
+            every = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(every, t)
+        return [float(e.item()) if raw else round(1e3 * float(e.item()), 4) for e in every]
 
     def kernel_time(fn, lo, hi, launches, ticks_per_launch):
         """The kernel's launch-to-launch period with the queue pre-filled (a spin kernel holds the
@@ -742,6 +763,7 @@ def main():
         "vs_baseline": None,
         "dtype": "int32+f32 (reward f64)",
         "data": "synthetic (splitmix64 self-play actions in HBM)",
+        "library": library_info(),
         "config": {"workload": ("C4 strong: %d arenas over %d GPUs" % (N * world, world) if args.global_envs else
                                 "C3: %d arenas/GPU" % N) + ", self-play random actions, P2 external, auto-reset same-step",
                    "envs_per_gpu": N, "global_envs": N * world, "mode": args.mode,
@@ -791,6 +813,70 @@ def main():
                                   "note": "fs_step_rec + the records of every rank gathered to rank 0 "
                                           "only (grouped send / recv over RCCL, parallel.gather_records_to)"},
     }
+    # BASELINE configs[3] (C4): 262 144 arenas split over the N ranks (strong scaling), so the
+    # driver's plain `bench.py --gpus N` at N = 1, 2, 4, 8 records C4's scaling curve -- its N = 1
+    # point is all 262 144 arenas on one GPU.  Each rank: a second handle over its contiguous global
+    # range (arena_base, so seeds and hashed rows are the unsharded run's), the packed fused kernel
+    # timed at the headline's launch shape (R regions of --steps) and in LEG_TICKS-tick launches
+    # (R regions), barrier + max over ranks like the headline; no data-path collective.
+    if not args.no_c4 and c4_split(world, rank) is None:
+        out["c4_strong"] = {"skipped": "%d ranks do not split %d arenas evenly" % (world, C4_GLOBAL_ENVS)}
+    elif not args.no_c4:
+        c4n, c4b = c4_split(world, rank)
+        try:
+            sim4 = FootsiesSim(c4n, device=local, p2_mode="external", seed=0, arena_base=c4b)
+            rows4 = max(W + R * K, (R + 1) * LEG_TICKS)
+            a41, a42 = sim4.hash_actions(rows4, seed=args.seed, t0=0)
+            ch4 = chunk if args.mode == "fused" else 1
+            tr4 = sim4.alloc_packed_trajectory(max(ch4, LEG_TICKS))
+            _, f4 = make_runs(a41, a42, tr4, ch4, packed=True, handle=sim4.handle, n=c4n)
+            _, f4k = make_runs(a41, a42, tr4, LEG_TICKS, packed=True, handle=sim4.handle, n=c4n)
+            torch.cuda.synchronize(dev)
+            f4(0, max(1, W))
+            torch.cuda.synchronize(dev)
+            local_walls = []
+            w4 = [timed(f4, W + r * K, K) for r in range(R)]
+            wall4, mine4 = sorted(w4)[R // 2], sorted(local_walls)[R // 2]
+            f4k(0, LEG_TICKS)
+            torch.cuda.synchronize(dev)
+            local_walls = []
+            wk = [timed(f4k, (r + 1) * LEG_TICKS, LEG_TICKS) for r in range(R)]
+            wallk, minek = sorted(wk)[R // 2], sorted(local_walls)[R // 2]
+            kt4, km4 = kernel_time(f4k, LEG_TICKS, rows4, 5, LEG_TICKS)
+            kts4, kms4 = kernel_time(f4, W, W + R * K, max(5, args.kernel_samples // 5), ch4)
+            kname4 = L.fs_step_kernel(sim4.handle, LEG_TICKS, _abi.FS_KERNEL_PACKED).decode()
+            skname4 = L.fs_step_kernel(sim4.handle, ch4, _abi.FS_KERNEL_PACKED).decode()
+            b4 = c4n * (STATE_BYTES + LEG_TICKS * STEP_IO_BYTES)
+            bs4 = c4n * (STATE_BYTES + ch4 * STEP_IO_BYTES)
+            tr4k = pmc_traffic(kname4, c4n, LEG_TICKS)
+            out["c4_strong"] = {
+                "global_envs": C4_GLOBAL_ENVS, "scaling": "strong", "envs_per_gpu": c4n,
+                "envs_per_rank": [c4n] * world, "arena_base_per_rank": [int(e) for e in rank_values(float(c4b), raw=True)],
+                "value": C4_GLOBAL_ENVS * K / wall4, "unit": "env-steps/s", "ms_per_step": 1e3 * wall4 / K,
+                "steps": K, "ticks_per_launch": ch4, "region_walls_ms": [round(1e3 * w, 4) for w in w4],
+                "rank_walls_ms": rank_values(mine4), "kernel": skname4,
+                "kernel_avg_launch_us": kts4 * 1e6, "kernel_median_launch_us": kms4 * 1e6,
+                "frac": bs4 / kts4 / 1e9 / HBM_PEAK_GBPS,
+                "launch_%d" % LEG_TICKS: {
+                    "value": C4_GLOBAL_ENVS * LEG_TICKS / wallk, "ms_per_step": 1e3 * wallk / LEG_TICKS,
+                    "ticks_per_launch": LEG_TICKS, "region_walls_ms": [round(1e3 * w, 4) for w in wk],
+                    "rank_walls_ms": rank_values(minek), "kernel": kname4,
+                    "avg_launch_us": kt4 * 1e6, "median_launch_us": km4 * 1e6,
+                    "algorithmic_bytes_per_launch": b4, "achieved": b4 / kt4 / 1e9,
+                    "frac": b4 / kt4 / 1e9 / HBM_PEAK_GBPS,
+                    "traffic": tr4k[0] if tr4k else None, "traffic_source": tr4k[1] if tr4k else None},
+                "config": "C4 strong: %d arenas over %d GPU(s), %d per GPU (arena_base = rank x %d), self-play "
+                          "random actions, P2 external, packed trajectories (fs_step_n_packed)"
+                          % (C4_GLOBAL_ENVS, world, c4n, c4n),
+                "note": "value = all ranks' arenas x steps over the max-over-ranks median region of `steps` steps at "
+                        "the headline's launch shape; launch_%d: the same in %d-tick launches; frac: the kernel's "
+                        "algorithmic bytes per launch over its back-to-back launch period, against 8 TB/s"
+                        % (LEG_TICKS, LEG_TICKS)}
+            sim4.close()
+            del a41, a42, tr4, f4, f4k
+            torch.cuda.empty_cache()
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            out["c4_strong"] = {"error": "%s: %s" % (type(e).__name__, e)}
     # the fused legs beside the headline, on every rank (barrier + max over ranks, like the
     # headline), at a fixed shape whatever --steps is: R regions of LEG_TICKS ticks in
     # LEG_TICKS-tick launches, the median reported

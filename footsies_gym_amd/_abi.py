@@ -6,13 +6,14 @@ the test-side oracle binding (``oracle/binding.py``) agree on layouts.
 """
 import ctypes as C
 
-FS_ABI_VERSION = 6
+FS_ABI_VERSION = 7
 
 FS_OK = 0
 FS_E_INVALID = -1
 FS_E_DEVICE = -2
 FS_E_UNSUPPORTED = -3
 FS_E_OOM = -4
+FS_E_RUNTIME = -5
 
 FS_P2_EXTERNAL = 0
 FS_P2_BOT = 1
@@ -155,6 +156,8 @@ class fs_arena_state(C.Structure):
 # functions exported by libfootsies.so: name -> (restype, argtypes)
 LIB_FUNCTIONS = {
     "fs_abi_version": (C.c_int, []),
+    "fs_runtime_images": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "fs_runtime_version": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "fs_create": (C.c_int, [C.POINTER(fs_config), C.POINTER(C.c_void_p)]),
     "fs_reset": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "fs_set_p2_mode": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),

@@ -6,6 +6,8 @@
 // see fs_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+#include <link.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -168,9 +170,60 @@ int staging_wait(fs_context* h) {
   return FS_OK;
 }
 
+// The HIP / HSA runtime images mapped into this process (dl_iterate_phdr), "hip:" / "hsa:" + path
+// per line.  Two images of one runtime (e.g. /opt/rocm's libamdhip64 beside the copy bundled with
+// a torch wheel, mapped by an extension loaded before torch) each see their own device list, and
+// the one this library bound to reports no device (profiles/r05q_lib_before_torch.log).
+struct RuntimeImages {
+  std::vector<std::string> hip, hsa;
+};
+
+int collect_image(struct dl_phdr_info* info, size_t, void* arg) {
+  auto* r = static_cast<RuntimeImages*>(arg);
+  const char* path = info->dlpi_name;
+  if (!path || !*path) return 0;
+  const char* base = strrchr(path, '/');
+  base = base ? base + 1 : path;
+  auto add = [&](std::vector<std::string>& v) {
+    char real[4096];
+    std::string p = realpath(path, real) ? std::string(real) : std::string(path);
+    if (std::find(v.begin(), v.end(), p) == v.end()) v.push_back(p);
+  };
+  if (!strncmp(base, "libamdhip64.so", 14)) add(r->hip);
+  else if (!strncmp(base, "libhsa-runtime64.so", 19)) add(r->hsa);
+  return 0;
+}
+
+RuntimeImages runtime_images() {
+  RuntimeImages r;
+  dl_iterate_phdr(collect_image, &r);
+  return r;
+}
+
 }  // namespace
 
 FS_API int fs_abi_version(void) { return FS_ABI_VERSION; }
+
+FS_API int fs_runtime_images(char* buf, size_t len) {
+  RuntimeImages r = runtime_images();
+  std::string s;
+  for (auto& p : r.hip) s += "hip:" + p + "\n";
+  for (auto& p : r.hsa) s += "hsa:" + p + "\n";
+  if (buf && len) {
+    size_t n = std::min(len - 1, s.size());
+    memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return (int)std::max(r.hip.size(), r.hsa.size());
+}
+
+FS_API int fs_runtime_version(int* runtime, int* build) {
+  if (build) *build = HIP_VERSION;
+  int v = 0;
+  hipError_t e = hipRuntimeGetVersion(&v);
+  if (runtime) *runtime = e == hipSuccess ? v : 0;
+  return e == hipSuccess ? FS_OK : set_err(nullptr, FS_E_DEVICE, "hipRuntimeGetVersion: %s", hipGetErrorString(e));
+}
 
 FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
   g_create_error.clear();
@@ -190,8 +243,18 @@ FS_API int fs_create(const fs_config* cfg, fs_handle* out) {
                    cfg->frame_delay);
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
-  if (e != hipSuccess || ndev <= 0)
+  if (e != hipSuccess || ndev <= 0) {
+    RuntimeImages r = runtime_images();
+    if (r.hip.size() > 1 || r.hsa.size() > 1) {
+      const std::vector<std::string>& v = r.hip.size() > 1 ? r.hip : r.hsa;
+      return set_err(nullptr, FS_E_RUNTIME,
+                     "two %s runtimes are loaded in this process (%s and %s): the one libfootsies bound to sees no "
+                     "device.  Load the HIP runtime the rest of the process uses first (import torch before "
+                     "libfootsies), or run with one ROCm installation",
+                     r.hip.size() > 1 ? "HIP" : "HSA", v[0].c_str(), v[1].c_str());
+    }
     return set_err(nullptr, FS_E_DEVICE, "no HIP device available (%s)", hipGetErrorString(e));
+  }
   if (cfg->device_id < 0 || cfg->device_id >= ndev)
     return set_err(nullptr, FS_E_INVALID, "device_id %d out of range (%d devices)", cfg->device_id, ndev);
 

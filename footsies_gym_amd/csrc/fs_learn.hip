@@ -272,9 +272,12 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     int64_t row = tile * kTile + lane;
     bool in_table = true;
     if (runs) {  // (a run entry outside the table reads nothing and adds nothing, as a padding row)
+      // the run index is bounded before it is shifted: a huge entry (>= 2^(63 - run_shift))
+      // would otherwise wrap back into [0, n_rows) and read real rows
       const int64_t mask = ((int64_t)1 << run_shift) - 1;
-      row = (run_cur << run_shift) | (row & mask);
-      in_table = run_cur >= 0 && row < n_rows;
+      in_table = run_cur >= 0 && run_cur <= ((n_rows - 1) >> run_shift);
+      row = in_table ? ((run_cur << run_shift) | (row & mask)) : 0;
+      in_table = in_table && row < n_rows;
     }
     const bool valid = lane < ns && in_table;  // rows past n: x = 0 and g3 = 0, so they add nothing
 

@@ -23,7 +23,7 @@ One iteration:
    E_a~behaviour[log p_bf16(a) - log p_fp32(a)] of KL(bf16 actor || fp32 actor), and
    `logp_abs_diff`, the mean |log p_bf16(a) - log p_fp32(a)|.  The fp32 log-probs come from
    fs_ppo_eval at fp32 FMAs (FS_PPO_FP32) whatever the learner's precision; the critic values and
-   the gradients use `learner_precision`.
+   the gradients use `learner_precision`, whatever `old_logp` is (`PPOTrainer.prepare`).
 4. The new actor weights are copied into the rollout's device buffers (no reallocation).
 
 Nothing leaves the GPU inside an iteration, and the simulator never waits on the host.
@@ -395,7 +395,9 @@ class PPOTrainer:
         self._next_first = feats[T]
         return feats, self.actions, tr["reward"], tr["terminated"]
 
-    def update(self, feats, actions, rewards, dones):
+    def prepare(self, feats, actions, rewards, dones):
+        """The sample table of one rollout: (rows [T*N][12] -- features, action, old log-prob,
+        advantage, return --, gap = behaviour log-prob - fp32 log-prob over the KL samples)."""
         torch = _torch()
         T, N = actions.shape
         M = T * N
@@ -407,9 +409,10 @@ class PPOTrainer:
             if self._grad is not None:  # the forward passes, GAE and the sample table
                 # old32 -- the fp32 reference the KL diagnostic and old_logp="fp32" are defined
                 # against -- always at fp32 FMAs, whatever the learner's precision; the critic values
-                # (GAE's baseline) at the learner's own precision
-                if nk == M:
-                    v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk, precision="fp32")
+                # (GAE's baseline) always at the learner's own precision, whatever old_logp is (one
+                # call serves both when the learner is fp32 and every sample needs its log-prob)
+                if nk == M and self._grad.precision == "fp32":
+                    v, old32 = self._grad.evaluate(feats.view(-1, N_FEATURES), a, nk)
                 else:
                     v, _ = self._grad.evaluate(feats.view(-1, N_FEATURES))
                     _, old32 = self._grad.evaluate(x[:nk].contiguous(), a, nk, precision="fp32", values=False)
@@ -426,6 +429,13 @@ class PPOTrainer:
                 adv = (adv - adv.mean()) / (adv.std() + 1e-8)
                 rows = torch.cat([x, a[:, None].float(), old[:, None], adv[:, None], ret.reshape(M, 1)], dim=1)  # [M, 12]
             gap = behav[:nk] - old32
+        return rows, gap
+
+    def update(self, feats, actions, rewards, dones):
+        torch = _torch()
+        T, N = actions.shape
+        M = T * N
+        rows, gap = self.prepare(feats, actions, rewards, dones)
         # Minibatches: a random permutation of runs of _SHUFFLE_CHUNK consecutive samples (one tick,
         # that many consecutive arenas) when they tile the batch, so each minibatch is gathered as
         # whole runs (row copies) instead of 2 M scattered rows; per-sample otherwise.
@@ -433,7 +443,7 @@ class PPOTrainer:
         runs = rows.view(M // C, C, rows.shape[1])
         nb = (M // C + self.minibatches - 1) // self.minibatches
         for _ in range(self.epochs):
-            perm = torch.randperm(M // C, device=x.device, generator=self.gen)
+            perm = torch.randperm(M // C, device=rows.device, generator=self.gen)
             for i in range(0, M // C, nb):
                 if self._grad is not None:  # fused forward + backward straight into .grad, the runs read in place
                     lm = self._grad(rows, self.clip, self.vf_coef, self.ent_coef, runs=perm[i:i + nb], run_len=C)

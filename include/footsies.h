@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 6
+#define FS_ABI_VERSION 7
 
 /* error codes */
 #define FS_OK 0
@@ -37,6 +37,7 @@ extern "C" {
 #define FS_E_DEVICE (-2)       /* HIP runtime failure / no device */
 #define FS_E_UNSUPPORTED (-3)  /* configuration not implemented */
 #define FS_E_OOM (-4)
+#define FS_E_RUNTIME (-5)      /* fs_create found no device and two HIP / HSA runtime images in the process */
 
 /* P2 controller (GameManager.cs:183-190: --p2-bot / remote actor; FE:234-247) */
 #define FS_P2_EXTERNAL 0  /* P2 action supplied every step (FE `opponent` callable / remote actor) */
@@ -202,6 +203,16 @@ typedef struct fs_context* fs_handle;
 
 /* Library / ABI version (FS_ABI_VERSION). */
 int fs_abi_version(void);
+
+/* The HIP and HSA runtime images mapped into this process, one "hip:<path>" / "hsa:<path>" line
+ * each, written NUL-terminated into buf (truncated to len); returns the larger of the two image
+ * counts (1 when the process holds one runtime).  fs_create returns FS_E_RUNTIME, naming both
+ * paths, when it finds no device and more than one image of either runtime (ABI 7). */
+int fs_runtime_images(char* buf, size_t len);
+
+/* The HIP runtime version the library is bound to (hipRuntimeGetVersion) and the HIP_VERSION it
+ * was compiled against, either pointer optional (ABI 7). */
+int fs_runtime_version(int* runtime, int* build);
 
 /* Create N arenas on a device and run the game-start sequence (BattleCore.Start
  * + first Stop->Intro->Fight ticks, BC:105-128, 176-200, 262-291) so they sit at

@@ -21,6 +21,7 @@ def declared_functions():
 
 @pytest.fixture(scope="module")
 def lib():
+    import torch  # noqa: F401 -- first, as _lib.lib() does: one HIP runtime in the process
     from footsies_gym_amd import build
     build.build()
     return C.CDLL(build.LIB)
@@ -141,3 +142,73 @@ def test_ppo_grad_runs_argument_checks():
     rp = C.cast(runs, C.c_void_p)
     for args in ((None, 4, 4, 0), (rp, 4, 0, 0), (rp, 4, 4, -1), (rp, 4, 4, 31), (rp, 4, 4, 3), (rp, 0, 4, 0)):
         assert call(*args) == _abi.FS_E_INVALID, args
+
+
+def _run(code):
+    import sys
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout
+
+
+def test_second_runtime_is_named_in_the_create_error():
+    """A second HSA runtime image mapped beside the one libfootsies bound to (what loading the library
+    before torch did on the MI355X box, profiles/r05q_lib_before_torch.log): fs_runtime_images lists
+    both, and fs_create -- which then sees no device -- returns FS_E_RUNTIME naming both paths instead
+    of "no ROCm-capable device".  Needs two distinct runtime files (torch's bundled copy and
+    /opt/rocm's); skipped where the image has one."""
+    import glob
+    import torch
+    tdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    rocm = sorted(glob.glob("/opt/rocm/lib/libhsa-runtime64.so.1.*"))
+    if not os.path.exists(os.path.join(tdir, "libhsa-runtime64.so")) or not rocm:
+        pytest.skip("one HSA runtime in this image")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible: fs_create would succeed on the bound runtime's device list")
+    out = _run("import ctypes as C, torch\n"
+               "C.CDLL(%r)\n"
+               "from footsies_gym_amd import _lib, _abi\n"
+               "L = _lib.lib()\n"
+               "print(repr(_lib.runtime_images()))\n"
+               "h = C.c_void_p()\n"
+               "print(L.fs_create(C.byref(_abi.fs_config(num_envs=4)), C.byref(h)), h.value)\n"
+               "print(L.fs_last_error(None).decode())\n" % rocm[-1])
+    images, rc, msg = out.strip().splitlines()[-3:]
+    assert images.count("hsa:") == 2, images
+    assert rc.split() == [str(_abi.FS_E_RUNTIME), "None"], rc
+    assert "two HSA runtimes" in msg and os.path.realpath(rocm[-1]) in msg and "torch" in msg, msg
+
+
+def test_library_loads_without_torch():
+    """The C-ABI binding does not need torch (the reference client needs only gymnasium): with torch
+    made unimportable, lib() loads the library on /opt/rocm's runtime, the host-only entry points
+    answer, library_info reports the in-tree library, and fs_create without a device fails loudly."""
+    out = _run("import sys; sys.modules['torch'] = None\n"
+               "import ctypes as C\n"
+               "from footsies_gym_amd import _lib, _abi\n"
+               "L = _lib.lib()\n"
+               "info = _lib.library_info()\n"
+               "print(info['override'], info['path'], info['hip_build'] > 0)\n"
+               "h = C.c_void_p()\n"
+               "print(L.fs_create(C.byref(_abi.fs_config(num_envs=4)), C.byref(h)))\n"
+               "print('torch' in sys.modules and sys.modules['torch'] is not None)\n")
+    lines = out.strip().splitlines()[-3:]
+    assert lines[0] == "False footsies_gym_amd/libfootsies.so True", lines
+    assert int(lines[1]) in (_abi.FS_E_DEVICE, _abi.FS_OK), lines
+    assert lines[2] == "False"
+
+
+def test_library_override_is_reported(tmp_path):
+    """FOOTSIES_LIB (kernel A/B experiments) swaps the library loudly: a note on stderr and
+    library_info()['override'] (bench.py carries it in its line)."""
+    import shutil
+    import sys
+    from footsies_gym_amd import build
+    build.build()
+    alt = tmp_path / "libfootsies.so"
+    shutil.copy(build.LIB, alt)
+    r = subprocess.run([sys.executable, "-c", "from footsies_gym_amd import _lib; print(_lib.library_info()['override'])"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=dict(os.environ, FOOTSIES_LIB=str(alt)))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[-1] == "True"
+    assert "FOOTSIES_LIB overrides" in r.stderr

@@ -27,7 +27,28 @@ def json_line(stdout):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("gpus", [2, 3])
+def check_c4_plan(out, gpus):
+    """The c4_strong leg (BASELINE configs[3]) on every rank of the plain `bench.py --gpus N`:
+    262 144 / N arenas per rank over contiguous global ranges, arena_base = rank x 262 144 / N."""
+    c4 = out["c4_strong"]
+    assert c4["global_envs"] == 262144 and c4["scaling"] == "strong"
+    assert c4["envs_per_rank"] == [262144 // gpus] * gpus
+    assert c4["arena_base_per_rank"] == [r * (262144 // gpus) for r in range(gpus)]
+    assert sum(c4["envs_per_rank"]) == 262144
+
+
+def test_c4_split():
+    sys.path.insert(0, ROOT)
+    import bench
+    for world in (1, 2, 4, 8):
+        shards = [bench.c4_split(world, r) for r in range(world)]
+        assert [b for _, b in shards] == [r * 262144 // world for r in range(world)]
+        assert all(n == 262144 // world for n, _ in shards)
+        assert shards[-1][1] + shards[-1][0] == 262144
+    assert bench.c4_split(3, 0) is None  # no even split: the leg is skipped
+
+
+@pytest.mark.parametrize("gpus", [2, 3, 4])
 def test_gpus_n_launches_n_ranks(gpus):
     p = run_bench(["--gpus", str(gpus), "--dry-run", "--dist-backend", "gloo", "--steps", "20", "--regions", "3",
                    "--envs", "1000"])
@@ -38,6 +59,10 @@ def test_gpus_n_launches_n_ranks(gpus):
     assert out["ranks"]["world_size"] == gpus and out["ranks"]["backend"] == "gloo"
     assert len(out["ranks"]["rank_walls_ms"]) == gpus
     assert out["config"]["global_envs"] == gpus * 1000
+    if 262144 % gpus == 0:
+        check_c4_plan(out, gpus)
+    else:
+        assert out["c4_strong"]["envs_per_rank"] == [0] * gpus
     # whole-job rate: every rank's arenas x steps over the max-over-ranks median region
     wall_s = out["ms_per_step"] * out["steps"] / 1e3
     assert out["value"] == pytest.approx(gpus * 1000 * out["steps"] / wall_s, rel=1e-9)
@@ -51,6 +76,7 @@ def test_single_rank_needs_no_launcher():
     assert p.returncode == 0, p.stderr[-2000:]
     out = json_line(p.stdout)
     assert out["n_gpus"] == 1 and out["ranks"]["world_size"] == 1
+    check_c4_plan(out, 1)  # the curve's first point: all 262 144 arenas on one GPU
 
 
 def test_world_size_must_match_gpus():
@@ -92,6 +118,7 @@ def test_eight_ranks_dry_run():
     out = json_line(p.stdout)
     assert out["n_gpus"] == 8 and out["ranks"]["world_size"] == 8 and len(out["ranks"]["rank_walls_ms"]) == 8
     assert out["config"]["global_envs"] == 8 * 500
+    check_c4_plan(out, 8)
     wall_s = out["ms_per_step"] * out["steps"] / 1e3
     assert out["value"] == pytest.approx(8 * 500 * out["steps"] / wall_s, rel=1e-9)
 

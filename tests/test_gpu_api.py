@@ -478,15 +478,30 @@ def test_pack_outputs_kernel_matches_host_packing():
     (777, dict(p2_mode="bot", p1_mode="bot", autoreset_mode="next_step")),
     (3, dict(p2_mode="external")),  # few arenas: host actions travel in the kernel arguments
     (513, dict(p2_mode="external", frame_delay=2)),  # the delayed queue: fs_step + fs_pack_outputs
+    (2049, dict(p2_mode="external", geom=True)),  # general-geometry tick: y, -0.0 y, flipped
+    (1500, dict(p2_mode="bot", geom=True)),
 ])
 def test_step_rec_equals_step_then_pack(n, kw):
     """fs_step_rec (k_step writes the 40-byte gather records itself) == fs_step followed by
     fs_pack_outputs, byte for byte, on twin handles over 400 steps with terminal and reset rows,
-    and the outputs the handle keeps are the same as well."""
+    and the outputs the handle keeps are the same as well.  `geom`: both handles first load the
+    same arbitrary states with fighters off the ground (some at y = -0.0) and flipped facings, so
+    the steps run env_step<..., GEOM> and its record stores (write_record under GEOM)."""
+    import numpy as np
     import torch
     from footsies_gym_amd import parallel
     from footsies_gym_amd.simulator import FootsiesSim
+    from tests.parity_utils import random_states
+    kw = dict(kw)
+    geom = kw.pop("geom", False)
     a, b = FootsiesSim(n, seed=4, **kw), FootsiesSim(n, seed=4, **kw)
+    if geom:
+        st = random_states(n, np.random.default_rng(77), p2=kw["p2_mode"], geom_frac=0.3)
+        st["f"]["position_y"][::17, 0] = np.float32(-0.0)
+        assert (st["f"]["position_y"] != 0).any() and (st["f"]["facing_flipped"] == 1).any()
+        assert np.signbit(st["f"]["position_y"][::17, 0]).all()
+        a.set_state(st)
+        b.set_state(st)
     p1, p2 = a.hash_actions(400, seed=13)
     host = n <= 8
     terminals = 0

@@ -142,11 +142,20 @@ def test_ppo_grad_over_runs_equals_gathered_rows(precision, run_len, n_runs):
     grad_g = pg.grad.clone()
     loss_r = pg(rows, 0.2, 0.5, 0.01, runs=runs, run_len=run_len).clone()
     assert torch.equal(grad_g, pg.grad) and torch.equal(loss_g, loss_r)
-    # a run entry past the table: nothing read, nothing added (the padding rows' zero gradient)
-    bad = runs.clone()
-    bad[-1] = total // run_len + 5
-    pg(rows, 0.2, 0.5, 0.01, runs=bad, run_len=run_len)
-    assert bool(torch.isfinite(pg.grad).all())
+    # a run entry past the table: nothing read, nothing added (the padding rows' zero gradient) --
+    # whatever the entry: just past the table, negative, or so large that shifting it by the run
+    # length wraps back into the table (1 << 62 at run_len 2048 shifted to row 0)
+    outs = []
+    for v in (total // run_len + 5, -1, 1 << 62, (1 << 63) - 1):
+        bad = runs.clone()
+        bad[-1] = v
+        loss_b = pg(rows, 0.2, 0.5, 0.01, runs=bad, run_len=run_len).clone()
+        assert bool(torch.isfinite(pg.grad).all())
+        outs.append((loss_b, pg.grad.clone()))
+    for loss_b, grad_b in outs[1:]:
+        assert torch.equal(loss_b, outs[0][0]) and torch.equal(grad_b, outs[0][1])
+    if n_runs > 1:  # the padding run differs from the real run it replaced
+        assert not torch.equal(outs[0][1], grad_g)
     with pytest.raises(ValueError):
         pg(rows, 0.2, 0.5, 0.01, runs=runs, run_len=3)
     with pytest.raises(ValueError):

@@ -192,3 +192,26 @@ def test_ppo_iterations_learn_and_refresh_the_kernel_actor(N, horizon, iters, ol
         assert torch.equal(a, b.detach())
     assert any(not torch.equal(a, b) for a, b in zip(k0, tr.rollout.params))
     assert sim.steps_taken == iters * horizon
+
+
+@pytest.mark.parametrize("precision", ["split_bf16", "fp32"])
+def test_ppo_critic_values_do_not_depend_on_old_logp(precision):
+    """GAE's baseline (the critic values) comes from the learner's own precision whatever
+    old_logp is.  Two trainers from the same seed, one per old_logp mode, prepare the same rollout:
+    the advantages and returns (rows[:, 10:12]) agree bit for bit, the old log-prob column is the
+    behaviour log-prob in one and the fp32 recomputation in the other."""
+    import torch
+    from footsies_gym_amd.ppo import PPOTrainer
+    from footsies_gym_amd.simulator import FootsiesSim
+    got = {}
+    for old in ("behaviour", "fp32"):
+        sim = FootsiesSim(2048, p2_mode="bot", seed=5)
+        tr = PPOTrainer(sim, horizon=16, seed=3, old_logp=old, learner_precision=precision)
+        rows, gap = tr.prepare(*tr.collect())
+        torch.cuda.synchronize()
+        got[old] = (rows.clone(), tr.logp.reshape(-1).clone())
+        sim.close()
+    (rb, behav), (rf, behav2) = got["behaviour"], got["fp32"]
+    assert torch.equal(behav, behav2)  # the same rollout in both
+    assert torch.equal(rb[:, :9], rf[:, :9]) and torch.equal(rb[:, 10:12], rf[:, 10:12])
+    assert torch.equal(rb[:, 9], behav) and not torch.equal(rf[:, 9], behav)
