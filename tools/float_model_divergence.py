@@ -8,8 +8,10 @@ rounded on store (FS_FLOAT_DOUBLE).  Both are built and bit-exact between oracle
 measures how fast trajectories under the two models part.
 
 Per tick it reports the fraction of arenas whose canonical state (fs_arena_state, every field)
-differs, the fraction whose observation/info outputs differ, and the fraction that have differed at
-least once; per arena the first-divergence tick (its distribution) and whether it ever re-converged
+differs, the fraction whose observation/info outputs differ (the terminal record only on a terminal
+tick), the same excluding the positions (guard, move, frame, reward, termination ... -- what a
+discrete policy or the episode boundaries see), and the fraction that have differed at least once;
+per arena the first-divergence tick (its distribution) and whether it ever re-converged
 (the round start re-places both fighters, BC:279-286).  Test infrastructure (oracle/ only).
 
     python tools/float_model_divergence.py --envs 65536 --ticks 2000 --out profiles/r06_float_model_divergence.json
@@ -50,6 +52,8 @@ def main():
     first = np.full(n, -1, dtype=np.int64)        # first tick whose state differs
     first_obs = np.full(n, -1, dtype=np.int64)    # first tick whose outputs differ
     reconverged = np.zeros(n, dtype=bool)         # differed once, equal again later
+    first_disc = np.full(n, -1, dtype=np.int64)   # first tick whose non-position outputs differ
+    field_first, max_dpos = {}, 0.0
     series = []
     t0 = time.perf_counter()
     for t in range(T):
@@ -57,14 +61,28 @@ def main():
         double.step_n_hashed(1, a.seed)
         ds = (rows(strict.state()) != rows(double.state())).any(axis=1)
         os_, od = strict.outputs(copy=False), double.outputs(copy=False)
-        do = np.zeros(n, dtype=bool)
+        do = np.zeros(n, dtype=bool)       # this tick's observation / info / reward / flags differ
+        disc = np.zeros(n, dtype=bool)     # ... in a field other than the positions
+        term = (os_["terminated"] != 0) | (od["terminated"] != 0)
         for k in os_:
-            do |= (rows(os_[k].reshape(n, -1)) != rows(od[k].reshape(n, -1))).any(axis=1)
+            if k.startswith("final_"):     # the terminal record: only meaningful on a terminal tick
+                dk = term & (rows(os_[k].reshape(n, -1)) != rows(od[k].reshape(n, -1))).any(axis=1)
+            else:
+                dk = (rows(os_[k].reshape(n, -1)) != rows(od[k].reshape(n, -1))).any(axis=1)
+            if dk.any():
+                field_first.setdefault(k, t)
+            do |= dk
+            if k not in ("position", "final_position"):
+                disc |= dk
+        dp = np.abs(os_["position"].astype(np.float64) - od["position"].astype(np.float64)).max()
+        max_dpos = max(max_dpos, float(dp))
         first[(first < 0) & ds] = t
         first_obs[(first_obs < 0) & do] = t
+        first_disc[(first_disc < 0) & disc] = t
         reconverged |= (first >= 0) & ~ds
         if t % a.every == a.every - 1 or t == T - 1:
             series.append({"tick": t + 1, "state_differs": float(ds.mean()), "outputs_differ": float(do.mean()),
+                           "discrete_outputs_differ": float(disc.mean()),
                            "ever_differed": float((first >= 0).mean())})
     dt = time.perf_counter() - t0
     strict.close()
@@ -84,6 +102,10 @@ def main():
         "first_divergence_tick_histogram": {"edges": hist_edges[:-1] + ["inf"],
                                             "counts": np.histogram(ever, bins=hist_edges)[0].tolist()},
         "first_output_divergence_tick_percentiles": pct(first_obs[first_obs >= 0]),
+        "arenas_discrete_outputs_ever_differed": float((first_disc >= 0).mean()),
+        "first_discrete_divergence_tick_percentiles": pct(first_disc[first_disc >= 0]),
+        "first_tick_each_output_field_differed": field_first,
+        "max_abs_position_difference": max_dpos,
         "series": series,
         "refs": "F:300, 305, 316 (UpdateMovement), BC:492-498, 511-515 (pushes); DESIGN.md §3 Float model",
     }

@@ -25,7 +25,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "exp", "timeline")
+OUT = os.path.join(ROOT, "runs", "timeline")  # (git-ignored; travels to the GPU box)
 NSTAMP = 8  # u64 per wave: t0 t1 t2 t3 hwid xcc pad pad
 MAXWAVES = 16384
 
