@@ -398,7 +398,8 @@ def issue_profile(kernel, envs, ticks):
             doc = json.load(f)
         kernels = doc.get("kernels", []) if isinstance(doc, dict) else []
         for k in kernels if isinstance(kernels, list) else []:  # (other summaries have other layouts)
-            if isinstance(k, dict) and k.get("kernel") == kernel and k.get("envs") == envs:
+            if (isinstance(k, dict) and k.get("kernel") == kernel and k.get("envs") == envs
+                    and k.get("ticks_per_launch") == ticks):
                 pw = k["per_wave_tick"]
                 best = {"insts_per_wave_tick": round(k["insts_per_wave_tick"], 1),
                         "valu_per_wave_tick": round(pw.get("SQ_INSTS_VALU", 0.0), 1),
@@ -422,6 +423,19 @@ def issue_profile(kernel, envs, ticks):
                          "simd_cycles_per_valu_class": m["simd_cycles_per_valu"],
                          "model_source": os.path.relpath(path, ROOT)})
     return best
+
+
+def short_launch_attribution(ticks):
+    """The committed critical-path split of an isolated launch of `ticks` ticks
+    (profiles/*_t<ticks>_attribution.json, tools/short_launch_attribution.py over the stamped
+    timeline of tools/timeline_probe.py), or None."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_t%d_attribution.json" % ticks)))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        doc = json.load(f)
+    return dict(doc["critical_path"], span_us=doc["span_us"], source=os.path.relpath(paths[-1], ROOT))
 
 
 def dry_run(args, world, rank):
@@ -744,6 +758,8 @@ def main():
     st_kname = L.fs_step_kernel(h, chunk if args.mode == "fused" else 1, layout_flag if args.mode == "fused" else 0).decode()
     achieved = bytes_per_launch / kt / 1e9
     tr = pmc_traffic(kname, N, ticks)
+    st_ticks = chunk if args.mode == "fused" else 1
+    st_tr = pmc_traffic(st_kname, N, st_ticks)
     issue = issue_profile(kname, N, ticks)
     # what binds the kernel: its SIMDs' instruction issue when the committed issue model puts the
     # kernel nearer that limit than HBM's (the C3 kernel: 0.90 of its issue plateau, ~0.3 of HBM)
@@ -796,8 +812,11 @@ def main():
                                   "algorithmic_bytes_per_launch": st_bytes,
                                   "frac": st_bytes / st_kt / 1e9 / HBM_PEAK_GBPS,
                                   "kernel": st_kname,
-                                  "traffic": (pmc_traffic(st_kname, N, chunk if args.mode == "fused" else 1) or
-                                              (None,))[0]},
+                                  "traffic": (st_tr or (None,))[0],
+                                  "traffic_ratio": (st_tr[0] / st_bytes) if st_tr else None,
+                                  "traffic_source": st_tr[1] if st_tr else None,
+                                  "issue": issue_profile(st_kname, N, st_ticks),
+                                  "attribution": short_launch_attribution(st_ticks)},
         other + "_mode": {"value": res[other]["env_steps_per_s"], "ms_per_step": res[other]["ms_per_step"]},
         "fused_other_layout": other_layout,
         "host_actions_step_mode": {"value": world * host_rate, "steps": kh,
