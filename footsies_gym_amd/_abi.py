@@ -157,6 +157,9 @@ class fs_arena_state(C.Structure):
 LIB_FUNCTIONS = {
     "fs_abi_version": (C.c_int, []),
     "fs_runtime_images": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "fs_host_alloc": (C.c_int, [C.c_int, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "fs_host_free": (C.c_int, [C.c_void_p]),
+    "fs_memcpy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "fs_runtime_version": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "fs_create": (C.c_int, [C.POINTER(fs_config), C.POINTER(C.c_void_p)]),
     "fs_reset": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),

@@ -903,6 +903,43 @@ FS_API int fs_sync(fs_handle h) {
   return FS_OK;
 }
 
+// Pinned, device-mapped host memory for callers without a device-memory library of their own (the
+// torch-free Python surface binds its host outputs here): zero-filled, with its device address.
+FS_API int fs_host_alloc(int device, size_t bytes, void** host, void** dev) {
+  if (!host || !dev || !bytes) return set_err(nullptr, FS_E_INVALID, "fs_host_alloc: bytes > 0 and both pointers required");
+  *host = *dev = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return set_err(nullptr, FS_E_DEVICE, "fs_host_alloc: hipSetDevice(%d): %s", device, hipGetErrorString(e));
+  void* p = nullptr;
+  e = hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable);
+  if (e != hipSuccess) return set_err(nullptr, FS_E_OOM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  memset(p, 0, bytes);
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, p, 0);
+  if (e != hipSuccess || !d) {
+    (void)hipHostFree(p);
+    return set_err(nullptr, FS_E_DEVICE, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+  }
+  *host = p;
+  *dev = d;
+  return FS_OK;
+}
+
+FS_API int fs_host_free(void* host) {
+  if (!host) return FS_OK;
+  hipError_t e = hipHostFree(host);
+  return e == hipSuccess ? FS_OK : set_err(nullptr, FS_E_DEVICE, "hipHostFree: %s", hipGetErrorString(e));
+}
+
+// A synchronous copy between any two addresses the runtime knows (device, pinned host or pageable
+// host; hipMemcpyDefault), for the same callers.
+FS_API int fs_memcpy(void* dst, const void* src, size_t bytes) {
+  if (!bytes) return FS_OK;
+  if (!dst || !src) return set_err(nullptr, FS_E_INVALID, "fs_memcpy: null pointer");
+  hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyDefault);
+  return e == hipSuccess ? FS_OK : set_err(nullptr, FS_E_DEVICE, "fs_memcpy: %s", hipGetErrorString(e));
+}
+
 FS_API void* fs_stream(fs_handle h) { return h ? (void*)h->stream : nullptr; }
 FS_API int fs_set_stream(fs_handle h, void* stream) {
   if (!h) return FS_E_INVALID;

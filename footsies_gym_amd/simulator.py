@@ -4,6 +4,13 @@ PyTorch is used only as device-memory and stream plumbing: the output buffers ar
 torch tensors bound into the library (``fs_bind_outputs``) and the library runs
 on torch's current stream (``fs_set_stream``), so device-side actions produced
 by a policy and the observations consumed by it need no extra synchronisation.
+
+Without torch (``backend="native"``, the default when torch is not installed) a handle with
+``host_outputs`` still works: its outputs live in pinned host memory the library allocates
+(``fs_host_alloc``), actions come from host arrays, and the library issues on its own stream --
+what the numpy ``FootsiesVectorEnv`` / ``FootsiesEnv`` need, so a reference user with only numpy
+(and gymnasium) can step the simulator.  The device-tensor APIs (step_n, trajectories, torch
+outputs) need torch.
 """
 import ctypes as C
 
@@ -22,6 +29,14 @@ _TORCH_DTYPES = {"u1": "uint8", "f4": "float32", "f8": "float64", "i4": "int32"}
 
 def _torch():
     import torch
+    return torch
+
+
+def _torch_or_none():
+    try:
+        import torch
+    except ImportError:
+        return None
     return torch
 
 
@@ -60,9 +75,17 @@ class FootsiesSim:
 
     def __init__(self, num_envs, device=0, p2_mode="bot", dense_reward=True, float_mode="strict",
                  autoreset_mode="same_step", seed=0, frame_delay=0, p1_mode="external", arena_base=0,
-                 host_outputs=False):
-        torch = _torch()
-        if not torch.cuda.is_available():
+                 host_outputs=False, backend=None):
+        if backend not in (None, "torch", "native"):
+            raise ValueError("backend must be 'torch' or 'native'")
+        torch = _torch_or_none() if backend != "native" else None
+        if backend == "torch" and torch is None:
+            raise ImportError("FootsiesSim(backend='torch') needs PyTorch")
+        if torch is None and not host_outputs:
+            raise ImportError("FootsiesSim with device outputs needs PyTorch; without it use host_outputs=True "
+                              "(the numpy FootsiesVectorEnv / FootsiesEnv do)")
+        self._native = torch is None
+        if not self._native and not torch.cuda.is_available():
             raise RuntimeError("FootsiesSim needs a HIP device (torch.cuda.is_available() is False)")
         if p2_mode not in P2_MODES:
             raise ValueError("p2_mode must be one of %s" % list(P2_MODES))
@@ -73,8 +96,9 @@ class FootsiesSim:
         if p1_mode not in P1_MODES:
             raise ValueError("p1_mode must be one of %s" % list(P1_MODES))
         self.num_envs = int(num_envs)
-        self.device = torch.device("cuda", device)
-        self._dev_index = self.device.index
+        self.device = int(device) if self._native else torch.device("cuda", device)
+        self._dev_index = int(device) if self._native else self.device.index
+        self._host_mem = None
         self.p2_mode = p2_mode
         self.p1_mode = p1_mode
         self.autoreset_mode = autoreset_mode
@@ -103,36 +127,60 @@ class FootsiesSim:
         # outputs() then returns host tensors; every call that returns them (step, reset, step_n
         # without a trajectory, outputs) first waits for the handle's stream, so they never hold
         # an earlier tick's values while the kernels are still writing (_host_ready).
+        # (the pinned host buffer comes from the library, fs_host_alloc, which also gives its device
+        # address: no second HIP runtime is ever loaded by name from here)
         self.host_outputs = bool(host_outputs)
         if self.host_outputs:
-            self._out_buf = torch.zeros(total, dtype=torch.uint8, pin_memory=True)
+            hp, dp = C.c_void_p(), C.c_void_p()
+            rc = lib().fs_host_alloc(self._dev_index, total, C.byref(hp), C.byref(dp))
+            if rc:
+                lib().fs_destroy(h)
+                self._h = None
+                check(rc, None)
+            self._host_mem = hp.value
+            host = np.ctypeslib.as_array((C.c_uint8 * total).from_address(hp.value))
+            self._out_buf = host if self._native else torch.from_numpy(host)
+            base, host_base = dp.value, hp.value
         else:
             with torch.cuda.device(self.device):
                 self._out_buf = torch.zeros(total, dtype=torch.uint8, device=self.device)
+            base = host_base = self._out_buf.data_ptr()
         for name, dt, shape, off, nbytes in layout:
-            self._out[name] = self._out_buf[off:off + nbytes].view(getattr(torch, _TORCH_DTYPES[dt])).view(shape)
+            if self._native:
+                self._out[name] = self._out_buf[off:off + nbytes].view(dt).reshape(shape)
+            else:
+                self._out[name] = self._out_buf[off:off + nbytes].view(getattr(torch, _TORCH_DTYPES[dt])).view(shape)
         self._out_layout = layout
         self._host_buf = None  # pinned mirror of _out_buf, allocated on first use
         # the library's creation-time outputs (state(-1)) into the bound buffers
         own = _abi.fs_outputs()
         check(lib().fs_outputs_get(h, C.byref(own)), h)
         check(lib().fs_sync(h), h)
-        for name in _abi.OUTPUT_SPEC:
-            t = self._out[name]
-            _copy_device(t.data_ptr(), getattr(own, name), t.numel() * t.element_size())
-        # (pinned host buffers are bound through their device-side address, hipHostGetDevicePointer)
-        base = _host_device_pointer(self._out_buf.data_ptr()) if self.host_outputs else self._out_buf.data_ptr()
+        for name, dt, shape, off, nbytes in layout:
+            check(lib().fs_memcpy(C.c_void_p(host_base + off), C.c_void_p(getattr(own, name)), nbytes), None)
         bind = _abi.fs_outputs(**{name: base + off for name, _, _, off, _ in layout})
         check(lib().fs_bind_outputs(h, C.byref(bind)), h)
-        self.use_torch_stream()
+        if self._native:
+            self._stream = None  # the library's own stream
+        else:
+            self.use_torch_stream()
 
     # -- streams ---------------------------------------------------------------------
     def use_torch_stream(self, stream=None):
         """Issue all further work on ``stream`` (default: torch's current stream)."""
+        self._need_torch("use_torch_stream")
         torch = _torch()
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         check(lib().fs_set_stream(self._h, C.c_void_p(s.cuda_stream)), self._h)
         self._stream = s
+
+    def _need_torch(self, what):
+        if self._native:
+            raise RuntimeError("FootsiesSim.%s needs PyTorch (this handle runs without it: backend='native')" % what)
+
+    @property
+    def backend(self):
+        return "native" if self._native else "torch"
 
     @property
     def stream(self):
@@ -165,8 +213,16 @@ class FootsiesSim:
         host arrays ((N,3) bools or (N,) ints).  active: optional [N] mask -- only those arenas
         tick (fs_step_masked); the others keep their state and outputs.  With p1_mode="bot"
         (by_example) p1 is ignored and may be None."""
-        torch = _torch()
         ext = self.p2_mode == "external"
+        if self._native:  # host arrays only
+            if ext and p2 is None:
+                raise ValueError("p2 actions are required when p2_mode='external'")
+            if p1 is None:
+                if self.p1_mode != "bot":
+                    raise ValueError("p1 actions are required unless p1_mode='bot'")
+                p1 = np.zeros(self.num_envs, np.uint8)
+            return self._step_host(p1, p2 if ext else None, active)
+        torch = _torch()
         # the RL loop's case first: uint8 [N] contiguous tensors on this handle's GPU, no mask
         # (the ctypes prototype takes the raw pointers as ints; nothing is converted or copied)
         if active is None and _fast_actions(p1, self._dev_index, self.num_envs) and (
@@ -195,22 +251,28 @@ class FootsiesSim:
                 check(lib().fs_step_masked(self._h, C.c_void_p(p1.data_ptr()), q2, C.c_void_p(m.data_ptr()),
                                            _abi.FS_ACT_DEVICE), self._h)
         else:
-            a1 = np.ascontiguousarray(encode_actions(_host(p1)))
-            a2 = np.ascontiguousarray(encode_actions(_host(p2))) if ext else None
-            if a1.shape[0] != self.num_envs or (a2 is not None and a2.shape[0] != self.num_envs):
-                raise ValueError("expected %d actions" % self.num_envs)
-            q2 = None if a2 is None else a2.ctypes.data
-            if active is None:
-                check(lib().fs_step(self._h, a1.ctypes.data, q2, _abi.FS_ACT_HOST), self._h)
-            else:
-                m = np.ascontiguousarray(np.asarray(active).reshape(self.num_envs), dtype=np.uint8)
-                check(lib().fs_step_masked(self._h, a1.ctypes.data, q2, m.ctypes.data, _abi.FS_ACT_HOST), self._h)
+            return self._step_host(p1, p2 if ext else None, active)
+        return self._ready_out()
+
+    def _step_host(self, p1, p2, active):
+        """fs_step / fs_step_masked with host actions (FS_ACT_HOST: the library stages them)."""
+        a1 = np.ascontiguousarray(encode_actions(_host(p1)))
+        a2 = np.ascontiguousarray(encode_actions(_host(p2))) if p2 is not None else None
+        if a1.shape[0] != self.num_envs or (a2 is not None and a2.shape[0] != self.num_envs):
+            raise ValueError("expected %d actions" % self.num_envs)
+        q2 = None if a2 is None else a2.ctypes.data
+        if active is None:
+            check(lib().fs_step(self._h, a1.ctypes.data, q2, _abi.FS_ACT_HOST), self._h)
+        else:
+            m = np.ascontiguousarray(np.asarray(active).reshape(self.num_envs), dtype=np.uint8)
+            check(lib().fs_step_masked(self._h, a1.ctypes.data, q2, m.ctypes.data, _abi.FS_ACT_HOST), self._h)
         return self._ready_out()
 
     def _check_device(self, t, name, dtype, numel):
         """A buffer the kernels read or write through its raw pointer: a contiguous torch tensor of
         `dtype` on this handle's GPU with at least `numel` elements (anything else would hand the
         kernel a host or foreign-device address, or let it run past the end)."""
+        self._need_torch("_check_device")
         torch = _torch()
         if not (isinstance(t, torch.Tensor) and t.is_cuda and t.get_device() == self._dev_index and t.dtype == dtype
                 and t.is_contiguous() and t.numel() >= numel):
@@ -220,6 +282,7 @@ class FootsiesSim:
     def step_n(self, n, p1=None, p2=None, action_seed=0, trajectory=None):
         """n ticks in one kernel launch.  p1/p2: device uint8 [n][N] or None (on-device hashed
         actions).  trajectory: dict of device tensors shaped [n][N](,2) like ``alloc_trajectory``."""
+        self._need_torch("step_n")
         torch = _torch()
         n = int(n)
         for name, a in (("p1", p1), ("p2", p2)):
@@ -240,6 +303,7 @@ class FootsiesSim:
 
     def hash_actions(self, n_steps, seed=0x5EED, t0=0, p2=True):
         """Device uint8 [n_steps][N] action arrays from the synthetic splitmix64 stream."""
+        self._need_torch("hash_actions")
         torch = _torch()
         p1 = torch.empty((n_steps, self.num_envs), dtype=torch.uint8, device=self.device)
         q2 = torch.empty((n_steps, self.num_envs), dtype=torch.uint8, device=self.device) if p2 else None
@@ -251,6 +315,7 @@ class FootsiesSim:
         """Device buffers for step_n_packed: {"lanes": uint8 [n][N][2][16], "reward": float64
         [n][N], "final_lanes": uint8 [n][N][2][16] (same-step auto-reset only, else None)}
         (include/footsies.h fs_packed_traj); unpack_trajectory gives their per-field views."""
+        self._need_torch("alloc_packed_trajectory")
         torch = _torch()
         shape = (n, self.num_envs, 2, _abi.FS_PACKED_LANE_BYTES)
         same = self.autoreset_mode == "same_step"
@@ -261,6 +326,7 @@ class FootsiesSim:
     def step_n_packed(self, n, p1, p2=None, trajectory=None):
         """step_n with device action rows p1 / p2 (uint8 [n][N]) into a packed trajectory
         (fs_step_n_packed: two stores per tick instead of ten; alloc_packed_trajectory)."""
+        self._need_torch("step_n_packed")
         torch = _torch()
         n = int(n)
         traj = trajectory if trajectory is not None else self.alloc_packed_trajectory(n)
@@ -280,6 +346,7 @@ class FootsiesSim:
         return traj
 
     def alloc_trajectory(self, n):
+        self._need_torch("alloc_trajectory")
         torch = _torch()
         out = {}
         for name, (dt, cols) in _abi.OUTPUT_SPEC.items():
@@ -302,6 +369,7 @@ class FootsiesSim:
         """step() of every arena that also writes the step's 40-byte records (fs_step_rec: the
         bytes pack_outputs would, from the tick's own kernel); device uint8 [N] actions (p1 may
         be None with p1_mode="bot").  Returns the [N, 40] uint8 device records."""
+        self._need_torch("step_records")
         torch = _torch()
         if dst is None:
             dst = torch.empty((self.num_envs, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=self.device)
@@ -320,6 +388,7 @@ class FootsiesSim:
     def pack_outputs(self, dst=None):
         """The current outputs as one 40-byte record per arena ([N, 40] uint8 device tensor,
         parallel.RECORD_BYTES layout) by one kernel (fs_pack_outputs): the gather payload."""
+        self._need_torch("pack_outputs")
         torch = _torch()
         if dst is None:
             dst = torch.empty((self.num_envs, _abi.FS_RECORD_BYTES), dtype=torch.uint8, device=self.device)
@@ -331,11 +400,10 @@ class FootsiesSim:
         buffer.  copy=False returns views of that buffer, overwritten by the next call.
         (_synced, internal: with host_outputs, the caller has just waited for the stream --
         step / reset returned -- and nothing was issued since.)"""
-        torch = _torch()
         if self._host_buf is None:
             self._host_buf = (self._out_buf if self.host_outputs else
-                              torch.empty(self._out_buf.numel(), dtype=torch.uint8, pin_memory=True))
-            host = self._host_buf.numpy()
+                              _torch().empty(self._out_buf.numel(), dtype=_torch().uint8, pin_memory=True))
+            host = self._host_buf if self._native else self._host_buf.numpy()
             # the typed views of the pinned buffer, made once (building them costs ~20 us a call)
             self._host_views = {name: host[off:off + nbytes].view(dt).reshape(shape)
                                 for name, dt, shape, off, nbytes in self._out_layout}
@@ -345,6 +413,7 @@ class FootsiesSim:
         else:
             # on the handle's own stream, so the copy is ordered after the library's kernels whatever
             # torch's current stream is (a blocking copy: it returns once the bytes are on the host)
+            torch = _torch()
             with torch.cuda.stream(self._stream):
                 self._host_buf.copy_(self._out_buf)
         if copy:
@@ -384,6 +453,12 @@ class FootsiesSim:
             lib().fs_sync(self._h)
             lib().fs_destroy(self._h)
             self._h = None
+        if getattr(self, "_host_mem", None):
+            self._out = {}
+            self._host_views = {}
+            self._out_buf = self._host_buf = None
+            lib().fs_host_free(C.c_void_p(self._host_mem))
+            self._host_mem = None
 
     def __del__(self):
         try:
@@ -393,8 +468,8 @@ class FootsiesSim:
 
 
 def _host(a):
-    torch = _torch()
-    if isinstance(a, torch.Tensor):
+    torch = _torch_or_none()
+    if torch is not None and isinstance(a, torch.Tensor):
         return a.detach().cpu().numpy()
     return a
 
@@ -454,41 +529,3 @@ def _as_u8_device(t, n):
         raise ValueError("expected device actions of shape (%d,), got %s" % (n, tuple(t.shape)))
     return t
 
-
-_hip = None
-
-
-def _hip_lib():
-    global _hip
-    if _hip is None:
-        for name in ("libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"):
-            try:
-                _hip = C.CDLL(name)
-                break
-            except OSError:
-                continue
-        if _hip is None:
-            raise RuntimeError("libamdhip64 not found")
-        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-        _hip.hipMemcpy.restype = C.c_int
-        _hip.hipHostGetDevicePointer.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_uint]
-        _hip.hipHostGetDevicePointer.restype = C.c_int
-    return _hip
-
-
-def _host_device_pointer(host_ptr):
-    """The device-side address of pinned host memory (hipHostGetDevicePointer); an error, never a
-    guess, if the runtime has no mapping for it."""
-    d = C.c_void_p()
-    rc = _hip_lib().hipHostGetDevicePointer(C.byref(d), C.c_void_p(host_ptr), 0)
-    if rc != 0 or not d.value:
-        raise RuntimeError("pinned output buffer has no device mapping (hipHostGetDevicePointer: %d)" % rc)
-    return d.value
-
-
-def _copy_device(dst, src, nbytes):
-    """hipMemcpy from device memory to a bound output buffer (device, or pinned host with
-    host_outputs) through the HIP runtime (used once at construction)."""
-    rc = _hip_lib().hipMemcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, 4)  # hipMemcpyDefault (dst may be pinned host)
-    if rc != 0:
-        raise RuntimeError("hipMemcpy failed: %d" % rc)

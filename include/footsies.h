@@ -210,6 +210,14 @@ int fs_abi_version(void);
  * paths, when it finds no device and more than one image of either runtime (ABI 7). */
 int fs_runtime_images(char* buf, size_t len);
 
+/* Pinned, device-mapped host memory (hipHostMalloc, zero-filled) and its device address, for
+ * callers without a device-memory library of their own -- the torch-free Python surface binds its
+ * host outputs there (fs_bind_outputs takes *dev); fs_host_free releases it.  fs_memcpy is a
+ * synchronous copy between any two addresses the runtime knows (hipMemcpyDefault).  (ABI 7) */
+int fs_host_alloc(int device, size_t bytes, void** host, void** dev);
+int fs_host_free(void* host);
+int fs_memcpy(void* dst, const void* src, size_t bytes);
+
 /* The HIP runtime version the library is bound to (hipRuntimeGetVersion) and the HIP_VERSION it
  * was compiled against, either pointer optional (ABI 7). */
 int fs_runtime_version(int* runtime, int* build);

@@ -212,3 +212,23 @@ def test_library_override_is_reported(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.split()[-1] == "True"
     assert "FOOTSIES_LIB overrides" in r.stderr
+
+
+def test_native_backend_without_device_fails_loudly():
+    """FootsiesSim's torch-free backend: device outputs need torch (ImportError naming the way out);
+    with host outputs and no device, fs_create's error surfaces as FootsiesError -- no CPU fallback."""
+    out = _run("import sys; sys.modules['torch'] = None\n"
+               "from footsies_gym_amd.simulator import FootsiesSim\n"
+               "from footsies_gym_amd._lib import FootsiesError\n"
+               "try:\n"
+               "    FootsiesSim(8)\n"
+               "except ImportError as e:\n"
+               "    print('import-error', 'host_outputs=True' in str(e))\n"
+               "try:\n"
+               "    FootsiesSim(8, host_outputs=True)\n"
+               "    print('created')\n"
+               "except FootsiesError as e:\n"
+               "    print('footsies-error', e.code)\n")
+    lines = out.strip().splitlines()[-2:]
+    assert lines[0] == "import-error True", lines
+    assert lines[1] in ("footsies-error %d" % _abi.FS_E_DEVICE, "created"), lines
