@@ -867,7 +867,12 @@ def main():
             skname4 = L.fs_step_kernel(sim4.handle, ch4, _abi.FS_KERNEL_PACKED).decode()
             b4 = c4n * (STATE_BYTES + LEG_TICKS * STEP_IO_BYTES)
             bs4 = c4n * (STATE_BYTES + ch4 * STEP_IO_BYTES)
-            tr4k = pmc_traffic(kname4, c4n, LEG_TICKS)
+            # (a 1000-tick call at 262 144 arenas is two launches -- 32-bit trajectory offsets,
+            # fs_api.cpp kMaxPackedLaunchRows -- whose per-launch PMC summary is at ~500 ticks)
+            per_call = -(-LEG_TICKS // max(1, (0xFFFFFFFF // 32) // c4n))
+            tr4k = pmc_traffic(kname4, c4n, LEG_TICKS // per_call)
+            if tr4k:
+                tr4k = (tr4k[0] * per_call, tr4k[1])
             out["c4_strong"] = {
                 "global_envs": C4_GLOBAL_ENVS, "scaling": "strong", "envs_per_gpu": c4n,
                 "envs_per_rank": [c4n] * world, "arena_base_per_rank": [int(e) for e in rank_values(float(c4b), raw=True)],
@@ -883,7 +888,8 @@ def main():
                     "avg_launch_us": kt4 * 1e6, "median_launch_us": km4 * 1e6,
                     "algorithmic_bytes_per_launch": b4, "achieved": b4 / kt4 / 1e9,
                     "frac": b4 / kt4 / 1e9 / HBM_PEAK_GBPS,
-                    "traffic": tr4k[0] if tr4k else None, "traffic_source": tr4k[1] if tr4k else None},
+                    "traffic": tr4k[0] if tr4k else None, "traffic_ratio": (tr4k[0] / b4) if tr4k else None,
+                    "traffic_source": tr4k[1] if tr4k else None},
                 "config": "C4 strong: %d arenas over %d GPU(s), %d per GPU (arena_base = rank x %d), self-play "
                           "random actions, P2 external, packed trajectories (fs_step_n_packed)"
                           % (C4_GLOBAL_ENVS, world, c4n, c4n),
