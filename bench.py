@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--roofline-ticks", type=int, default=1000,
                     help="ticks per fs_step_n launch of the roofline block (the shape profiles/ covers)")
     ap.add_argument("--no-extras", action="store_true", help="skip the C2 bot-opponent and C5 policy-loop rates")
+    ap.add_argument("--no-solo-group", action="store_true",
+                    help="a plain one-GPU run stays without a process group (default: a one-rank RCCL group, so the "
+                         "per-step gather legs run their collective at N = 1 too)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the c4_strong leg (262 144 arenas split over the ranks, BASELINE configs[3])")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -454,9 +457,9 @@ def dry_run(args, world, rank):
         t0 = time.perf_counter()
         for _ in range(K):
             x.add_(1.0)
+        local.append(time.perf_counter() - t0)
         if world > 1:
             dist.barrier()
-        local.append(time.perf_counter() - t0)
         t = torch.tensor([local[-1]], dtype=torch.float64)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -510,6 +513,7 @@ def main():
     # a process group whenever a launcher started the ranks, a single one included (the driver's
     # torch.distributed.run at N = 1, or tests/test_gpu_rccl.py): RCCL then carries the barrier,
     # the max-over-ranks and the gather modes at every N
+    solo_group_error = None
     grouped = world > 1 or "WORLD_SIZE" in os.environ
     if grouped:
         torch.cuda.set_device(local)
@@ -517,6 +521,17 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    elif args.dist_backend == "nccl" and not args.no_solo_group:
+        # the plain one-GPU run (the driver's `bench.py --gpus 1`) joins a one-rank RCCL group too, so
+        # the per-step gather legs run their collective at N = 1 as well (RCCL's own kernels and
+        # copies at world size 1); a failure to form it leaves the run ungrouped and says so
+        torch.cuda.set_device(local)
+        try:
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % free_port(), rank=0, world_size=1,
+                                    device_id=torch.device("cuda", local))
+            grouped = True
+        except Exception as e:  # noqa: BLE001 - reported, never fatal to the headline
+            solo_group_error = "%s: %s" % (type(e).__name__, e)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo reduces host tensors
@@ -589,19 +604,22 @@ def main():
     base1, base2 = p1.data_ptr(), p2.data_ptr()
 
     def barrier():
-        if grouped:
+        if grouped and world > 1:  # (one rank has no one to wait for)
             dist.barrier()
 
     def timed(fn, k0, n):
-        """One timed region of exactly n steps: barrier + synchronize on both sides, host
-        wall clock, max over ranks.  Nothing else is issued inside the region."""
+        """One timed region of exactly n steps: barrier + synchronize on both sides, each rank's
+        host wall clock from its synchronize before the launches to its synchronize after them,
+        max over ranks.  Nothing else is issued inside the region; the closing barrier follows
+        the clock, so the collective's own latency is not counted as work (the max over ranks
+        holds the slowest rank's region)."""
         barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         fn(k0, n)
         torch.cuda.synchronize(dev)
-        barrier()
         wall = time.perf_counter() - t0
+        barrier()
         local_walls.append(wall)
         t = torch.tensor([wall], dtype=torch.float64, device=coll_dev)
         if grouped:
@@ -788,6 +806,7 @@ def main():
                    if args.mode == "fused" else None, "parallelism": "arena-shard x%d" % world},
         "ranks": {"world_size": dist.get_world_size() if grouped else 1,
                   "backend": dist.get_backend() if grouped else None,
+                  "launcher": "WORLD_SIZE" in os.environ, "solo_group_error": solo_group_error,
                   "rank_walls_ms": res[args.mode]["rank_walls_ms"],
                   "note": "world_size / backend as the process group reports them (nccl = RCCL); each rank's "
                           "median region wall, before the max over ranks"},
@@ -824,9 +843,10 @@ def main():
                                            "the gather legs: one untimed call, then the median of `regions` regions"},
         "step_gather_mode": {"value": world * N * kg / gwall, "ms_per_step": 1e3 * gwall / kg, "steps": kg,
                              "bytes_gathered_per_step": world * N * _abi.FS_RECORD_BYTES,
+                             "collective": bool(grouped and args.dist_backend == "nccl"),
                              "note": "fs_step_rec (records from the step kernel) + one all_gather_into_tensor of the 40-B "
-                                     "(obs, reward, done) records over RCCL per step (none without a process group -- a plain "
-                                     "1-GPU run -- or with --dist-backend gloo)"},
+                                     "(obs, reward, done) records over RCCL per step (at N = 1 in a one-rank RCCL group; "
+                                     "none with --no-solo-group or --dist-backend gloo)"},
         "step_gather_root_mode": {"value": world * N * kg / grwall, "ms_per_step": 1e3 * grwall / kg, "steps": kg,
                                   "bytes_into_rank0_per_step": (world - 1) * N * _abi.FS_RECORD_BYTES,
                                   "note": "fs_step_rec + the records of every rank gathered to rank 0 "
