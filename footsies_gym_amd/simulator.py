@@ -137,8 +137,10 @@ class FootsiesSim:
                 lib().fs_destroy(h)
                 self._h = None
                 check(rc, None)
-            self._host_mem = hp.value
-            host = np.ctypeslib.as_array((C.c_uint8 * total).from_address(hp.value))
+            self._host_mem = _HostBuffer(hp.value)
+            raw = (C.c_uint8 * total).from_address(hp.value)
+            raw._owner = self._host_mem  # every view of the buffer keeps it allocated (freed with the last)
+            host = np.frombuffer(raw, dtype=np.uint8)
             self._out_buf = host if self._native else torch.from_numpy(host)
             base, host_base = dp.value, hp.value
         else:
@@ -454,16 +456,31 @@ class FootsiesSim:
             lib().fs_destroy(self._h)
             self._h = None
         if getattr(self, "_host_mem", None):
+            # (the pinned buffer is freed when its last view is gone: outputs_numpy(copy=False) views
+            # a caller still holds stay readable, no longer written)
             self._out = {}
             self._host_views = {}
             self._out_buf = self._host_buf = None
-            lib().fs_host_free(C.c_void_p(self._host_mem))
             self._host_mem = None
 
     def __del__(self):
         try:
             self.close()
         except Exception:
+            pass
+
+
+class _HostBuffer:
+    """Pinned host memory from fs_host_alloc, released by fs_host_free when the last numpy / torch
+    view of it goes away."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        try:
+            lib().fs_host_free(C.c_void_p(self.ptr))
+        except Exception:  # (interpreter shutdown)
             pass
 
 

@@ -115,5 +115,12 @@ def test_native_backend_in_process_matches_torch_backend():
     for call in (lambda: a.hash_actions(4), lambda: a.alloc_trajectory(4), lambda: a.step_n(4)):
         with pytest.raises(RuntimeError, match="needs PyTorch"):
             call()
+    # views of the pinned outputs a caller still holds outlive close(): the buffer is released with
+    # the last of them, not under them
+    va, vb = a.outputs_numpy(copy=False)["position"], b.outputs_numpy(copy=False)["position"]
+    want = va.copy()
     a.close()
     b.close()
+    import gc
+    gc.collect()
+    assert va.tobytes() == want.tobytes() and vb.tobytes() == want.tobytes()
