@@ -129,10 +129,12 @@ def symbolize(obj, addrs):
 
 def line_marks(src_text):
     """env_step's stretches: (first line, phase) from ENV_STEP_MARKS, in source order."""
-    start = src_text.index("__device__ __forceinline__ void env_step(")
+    start = re.search(r"__device__ __forceinline__ \w+ env_step\(", src_text).start()
     out = []
     for needle, phase in ENV_STEP_MARKS:
-        k = src_text.index(needle, start)
+        k = src_text.find(needle, start)
+        if k < 0:  # (a mark of another revision's tick)
+            continue
         out.append((src_text.count("\n", 0, k) + 1, phase))
     return sorted(out)
 
