@@ -288,6 +288,32 @@ def ppo_rate(torch, N, device, horizon=128, iterations=3):
                       % (N, horizon)}
 
 
+def ppo_dp_rate(torch, N, device, rank, world, timed, horizon=128, iterations=3):
+    """Config C5 over the ranks as one job: data-parallel PPO, N arenas per rank (arena_base =
+    rank x N, P2 = bot), split-bf16 learner; each of the epochs x minibatches updates averages the
+    flat gradient buffer over the ranks (one all_reduce SUM over RCCL, parallel.allreduce_mean_)
+    and the advantages are normalised with every rank's statistics.  One untimed warm-up
+    iteration, then one timed region of `iterations` iterations (barrier + synchronize, max over
+    ranks); value = all ranks' samples / that wall."""
+    from footsies_gym_amd import _abi
+    from footsies_gym_amd.ppo import PPOTrainer
+    from footsies_gym_amd.simulator import FootsiesSim
+    sim = FootsiesSim(N, device=device, p2_mode="bot", seed=0, arena_base=rank * N)
+    tr = PPOTrainer(sim, horizon=horizon, group="default")
+    tr.train(1)
+    wall = timed(lambda k0, n: tr.train(n, sync=False), 0, iterations)
+    updates = tr.epochs * tr.minibatches
+    sim.close()
+    return {"value": world * N * horizon * iterations / wall, "unit": "env-steps/s",
+            "ms_per_iteration": 1e3 * wall / iterations, "horizon": horizon, "iterations": iterations,
+            "envs_per_rank": N, "allreduces_per_iteration": updates,
+            "allreduce_bytes": 4 * (_abi.FS_PPO_ACTOR_PARAMS + _abi.FS_PPO_CRITIC_PARAMS),
+            "config": "C5 data-parallel: %d ranks x %d arenas (P2 = bot), PPO with the fused rollout of %d ticks, "
+                      "GAE, %d Adam minibatch updates per iteration, each minibatch's gradient averaged over the "
+                      "ranks (all_reduce of the flat gradient buffer) and the advantages normalised with every "
+                      "rank's statistics" % (world, N, horizon, updates)}
+
+
 def vector_env_rate(torch, N, steps, device, warm=400):
     """The drop-in surface itself at the C3 size: FootsiesVectorEnv.step with numpy (N,) int
     actions in and numpy obs / reward / info out (the D2H copy, the conversions and gymnasium
@@ -962,6 +988,14 @@ def main():
             "frac": recv / (gowall / kg) / 1e9 / ((world - 1) * XGMI_LINK_GBPS),
             "note": "all_gather_into_tensor of every rank's [N, 40] records, alone (gather_only) and inside the "
                     "fs_step + pack + gather step (in_step); peak = one ~153 GB/s xGMI link per peer"}
+    # C5 at N > 1 as one training job: data-parallel PPO (ppo.PPOTrainer(group=...)), every rank
+    # rolling out its own N arenas (arena_base = rank x N) and averaging each minibatch's gradient
+    # over the ranks with one all_reduce; barrier + max over ranks around the iterations
+    if world > 1 and not args.no_extras:
+        try:
+            out["ppo_dp"] = ppo_dp_rate(torch, N, local, rank, world, timed)
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            out["ppo_dp"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if world == 1 and not args.no_extras:
         try:
             out["policy_loop"] = policy_loop_rate(torch, N, min(K, 1000), local)

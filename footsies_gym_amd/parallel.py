@@ -6,7 +6,9 @@ seeds, hashed actions and actor samples are keyed by the global index and any G
 produces the same per-arena trajectories.  The only collective is the optional
 per-step gather of (obs, reward, done) for a centralised learner: a packed 40-B
 per-arena record, all-gathered to every rank or gathered to one rank by grouped
-point-to-point sends over RCCL/xGMI.
+point-to-point sends over RCCL/xGMI.  Data-parallel PPO (ppo.PPOTrainer(group=...)) keeps its
+rollouts rank-local and averages each minibatch's gradient (`allreduce_mean_`) and the advantage
+statistics (`global_mean_std`) over the ranks.
 """
 import numpy as np
 
@@ -158,6 +160,41 @@ class ShardedSim:
 
     def close(self):
         self.sim.close()
+
+
+def allreduce_mean_(t, group=None):
+    """Data-parallel PPO's one exchange (rollouts stay rank-local, gradients are
+    averaged): `t` replaced in place by its mean over the ranks -- one all_reduce SUM over
+    RCCL / xGMI (through host memory with gloo), then / world.  Every rank ends with the same bits
+    (the collective's result is the same buffer on all of them).  Returns `t`."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if world == 1:
+        return t
+    x = _on_backend(t, group)
+    dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group)
+    x.div_(world)
+    if x is not t:
+        t.copy_(x)
+    return t
+
+
+def global_mean_std(x, group=None):
+    """Mean and unbiased standard deviation of the union of every rank's `x` (any shapes; ranks
+    may hold different counts), as a float32 [2] tensor on x's device: float64 sums, two
+    all_reduces of two scalars -- the global count and sum, then the squared deviations from the
+    global mean (the two-pass form torch.std uses on one tensor)."""
+    import torch
+    import torch.distributed as dist
+    xd = x.reshape(-1).double()
+    a = _on_backend(torch.stack([torch.tensor(float(xd.numel()), dtype=torch.float64, device=x.device), xd.sum()]),
+                    group)
+    dist.all_reduce(a, op=dist.ReduceOp.SUM, group=group)
+    n, mean = a[0].to(x.device), (a[1] / a[0]).to(x.device)
+    m2 = _on_backend(((xd - mean) ** 2).sum().reshape(1), group)
+    dist.all_reduce(m2, op=dist.ReduceOp.SUM, group=group)
+    std = (m2[0].to(x.device) / (n - 1)).sqrt()
+    return torch.stack([mean, std]).float()
 
 
 def global_seeds(global_envs, base_seed=0):

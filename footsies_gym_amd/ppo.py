@@ -307,17 +307,19 @@ def features_device(tr, out):
     return out
 
 
-def pack_rows(x, actions, old, adv, ret, out=None):
+def pack_rows(x, actions, old, adv, ret, out=None, stats=None):
     """fs_ppo_grad's [M, 12] sample table in one launch (fs_ppo_pack): x [M, 8] f32, actions u8
     [M], old log-probs, advantages and returns f32 [M]; the advantages normalised on the way as
-    (adv - mean) / (std + 1e-8) with torch's mean and (unbiased) std."""
+    (adv - mean) / (std + 1e-8) with torch's mean and (unbiased) std -- or with `stats` (a device
+    f32 [2]: mean, std), data-parallel PPO's statistics over every rank's advantages."""
     torch = _torch()
     M = x.shape[0]
     if (x.dtype != torch.float32 or tuple(x.shape) != (M, N_FEATURES) or actions.dtype != torch.uint8
             or not all(t.is_contiguous() and t.numel() == M for t in (actions, old, adv, ret))
             or not x.is_contiguous()):
         raise ValueError("pack_rows: contiguous x f32 [M, 8], actions u8 [M], old / adv / ret f32 [M]")
-    stats = torch.stack([adv.mean(), adv.std()])
+    if stats is None:
+        stats = torch.stack([adv.mean(), adv.std()])
     rows = out if out is not None else torch.empty((M, 12), dtype=torch.float32, device=x.device)
     stream = torch.cuda.current_stream(x.device).cuda_stream
     check(lib().fs_ppo_pack(C.c_void_p(x.data_ptr()), C.c_void_p(actions.data_ptr()), C.c_void_p(old.data_ptr()),
@@ -331,11 +333,21 @@ class PPOTrainer:
     rollout, all arenas in every minibatch round.  `learner_precision` is PPOGrad's: the
     split-bf16 hidden layer by default -- against a float64 autograd reference its gradients are
     within 5e-6 of each tensor's largest entry, as close as torch's own fp32 autograd (up to
-    1.1e-5; profiles/r04e_split_error.jsonl) -- or "fp32"."""
+    1.1e-5; profiles/r04e_split_error.jsonl) -- or "fp32".
+
+    Data-parallel (`group`: a torch.distributed process group, or "default" for the default one;
+    SURVEY.md §8(e)): one trainer per rank, each over its own FootsiesSim (a ShardedSim's handle:
+    its arena_base keys the actor's sampling stream, so ranks roll out different arenas), all with
+    the same `num_envs`.  The ranks start from rank 0's weights; rollouts, GAE and the sample table
+    stay rank-local, the advantages are normalised with the statistics of every rank's advantages
+    (parallel.global_mean_std), and each minibatch's gradient -- the mean over this rank's share of
+    it -- is averaged over the ranks (parallel.allreduce_mean_, one all_reduce of the flat gradient
+    buffer over RCCL) before the Adam step, so every rank applies the same update to the same
+    weights: G ranks x N arenas train one policy on G x N arenas' samples per iteration."""
 
     def __init__(self, sim, actor=None, critic=None, horizon=128, gamma=0.99, lam=0.95, epochs=2, minibatches=4,
                  lr=3e-4, clip=0.2, vf_coef=0.5, ent_coef=0.01, seed=0, old_logp="behaviour", learner="hip",
-                 kl_ticks=None, learner_precision="split_bf16"):
+                 kl_ticks=None, learner_precision="split_bf16", group=None):
         torch = _torch()
         if old_logp not in ("behaviour", "fp32"):
             raise ValueError("old_logp must be 'behaviour' or 'fp32'")
@@ -349,6 +361,13 @@ class PPOTrainer:
         self.sim = sim
         self.actor = actor if actor is not None else make_actor(device=dev, seed=seed)
         self.critic = critic if critic is not None else make_critic(device=dev, seed=seed + 1)
+        self.group, self.world = None, 1
+        if group is not None:
+            import torch.distributed as dist
+            self.group = None if group == "default" else group
+            self.world = dist.get_world_size(self.group)
+        if self.world > 1:
+            self._join_ranks(sim.num_envs)
         self.rollout = FusedPolicyRollout(sim, self.actor, seed=seed)
         self.horizon, self.gamma, self.lam = horizon, gamma, lam
         # the fp32 log-probs behind kl_behaviour_fp32 / logp_abs_diff: every tick when they are
@@ -370,6 +389,24 @@ class PPOTrainer:
         # the observation before the next rollout's first tick: the sim's outputs now, then
         # the last trajectory row (trajectory launches leave the regular outputs untouched)
         self._next_first = None
+
+    def _join_ranks(self, n):
+        """Data-parallel start: the same arena count on every rank (each minibatch step is one
+        collective per rank, so the ranks must take the same number of them) and rank 0's weights."""
+        import torch.distributed as dist
+        from .parallel import _on_backend
+        torch = _torch()
+        counts = [None] * self.world
+        dist.all_gather_object(counts, int(n), group=self.group)
+        if len(set(counts)) != 1:
+            raise ValueError("data-parallel PPO needs the same num_envs on every rank, got %s" % counts)
+        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        with torch.no_grad():
+            for p in list(self.actor.parameters()) + list(self.critic.parameters()):
+                b = _on_backend(p.data, self.group)
+                dist.broadcast(b, src, group=self.group)
+                if b is not p.data:
+                    p.data.copy_(b)
 
     def collect(self):
         """One fused rollout; returns (features [T+1][N][8] f32, actions u8, rewards f64, dones u8)
@@ -419,17 +456,46 @@ class PPOTrainer:
                 values = v.view(T + 1, N)
                 adv, ret = gae_device(rewards, dones, values, self.gamma, self.lam)
                 old = behav if self.old_logp == "behaviour" else old32
-                rows = pack_rows(x, a, old, adv.view(M), ret.view(M))
+                rows = pack_rows(x, a, old, adv.view(M), ret.view(M), stats=self._adv_stats(adv))
             else:
                 values = self.critic(feats).squeeze(-1)  # [T+1][N]
                 old32 = torch.log_softmax(self.actor(x[:nk]), dim=1).gather(1, a[:nk, None].long())[:, 0]
                 adv, ret = gae(rewards.float(), values, dones.float(), self.gamma, self.lam)
                 old = behav if self.old_logp == "behaviour" else old32
                 adv = adv.reshape(M)
-                adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+                st = self._adv_stats(adv)
+                if st is None:
+                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+                else:
+                    adv = (adv - st[0]) / (st[1] + 1e-8)
                 rows = torch.cat([x, a[:, None].float(), old[:, None], adv[:, None], ret.reshape(M, 1)], dim=1)  # [M, 12]
             gap = behav[:nk] - old32
         return rows, gap
+
+    def _adv_stats(self, adv):
+        """The advantage normalisation's (mean, std) over every rank (data-parallel), else None
+        (this rank's own, as pack_rows / the torch learner compute them)."""
+        if self.world == 1:
+            return None
+        from .parallel import global_mean_std
+        return global_mean_std(adv, self.group)
+
+    def _average_grads(self):
+        """Data-parallel: this minibatch's gradient averaged over the ranks before the step."""
+        if self.world == 1:
+            return
+        from .parallel import allreduce_mean_
+        if self._grad is not None:
+            allreduce_mean_(self._grad.grad, self.group)  # the flat buffer the .grad views share
+            return
+        torch = _torch()
+        ps = [p for p in list(self.actor.parameters()) + list(self.critic.parameters()) if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in ps])
+        allreduce_mean_(flat, self.group)
+        off = 0
+        for p in ps:
+            p.grad.copy_(flat[off:off + p.numel()].view_as(p.grad))
+            off += p.numel()
 
     def update(self, feats, actions, rewards, dones):
         torch = _torch()
@@ -447,6 +513,7 @@ class PPOTrainer:
             for i in range(0, M // C, nb):
                 if self._grad is not None:  # fused forward + backward straight into .grad, the runs read in place
                     lm = self._grad(rows, self.clip, self.vf_coef, self.ent_coef, runs=perm[i:i + nb], run_len=C)
+                    self._average_grads()
                     self.opt.step()
                     continue
                 b = runs[perm[i:i + nb]].view(-1, rows.shape[1])
@@ -463,11 +530,17 @@ class PPOTrainer:
                 loss = pg + self.vf_coef * vf - self.ent_coef * ent
                 self.opt.zero_grad(set_to_none=True)
                 loss.backward()
+                self._average_grads()
                 self.opt.step()
         self.rollout.refresh(self.actor)
         if self._grad is not None:
             pg, vf, ent = lm[0].clone(), lm[1].clone(), lm[2].clone()
             loss = pg + self.vf_coef * vf - self.ent_coef * ent
+        if self.world > 1:  # the last minibatch's losses, averaged like its gradient
+            from .parallel import allreduce_mean_
+            torch = _torch()
+            red = allreduce_mean_(torch.stack([loss.detach(), pg.detach(), vf.detach(), ent.detach()]), self.group)
+            loss, pg, vf, ent = red[0], red[1], red[2], red[3]
         self.stats = {"loss": loss.detach(), "policy_loss": pg.detach(), "value_loss": vf.detach(),
                       "entropy": ent.detach(), "mean_reward": rewards.mean(), "kl_behaviour_fp32": gap.mean(),
                       "logp_abs_diff": gap.abs().mean()}

@@ -95,3 +95,76 @@ def test_hashed_shards_are_g_invariant(oracle_lib, world):
         o.step_n_hashed(steps, 0xD15C)
         got.append(o.state())
     assert np.concatenate(got).tobytes() == want.tobytes()
+
+
+def dp_worker(rank, world, port, q):
+    """Data-parallel PPO's host logic over gloo on CPU (no simulator): global advantage statistics,
+    the gradient average and PPOTrainer's start (rank 0's weights, equal arena counts)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from footsies_gym_amd.parallel import allreduce_mean_, global_mean_std
+    from footsies_gym_amd.ppo import PPOTrainer, make_critic
+    from footsies_gym_amd.rollout import make_actor
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(1000 + 337 * rank, generator=g) * (1 + rank) + rank  # uneven shards
+    st = global_mean_std(x)
+    t = torch.randn(4801, generator=g)
+    mine = t.clone()
+    allreduce_mean_(t)
+    # PPOTrainer's data-parallel start and gradient average (the torch learner's path), without a sim
+    tr = PPOTrainer.__new__(PPOTrainer)
+    tr.group, tr.world, tr._grad = None, world, None
+    tr.actor, tr.critic = make_actor(seed=10 + rank), make_critic(seed=20 + rank)
+    tr._join_ranks(64)
+    w = torch.cat([p.detach().reshape(-1) for p in list(tr.actor.parameters()) + list(tr.critic.parameters())])
+    grads = []
+    for p in list(tr.actor.parameters()) + list(tr.critic.parameters()):
+        p.grad = torch.randn(p.shape, generator=g)
+        grads.append(p.grad.clone().reshape(-1))
+    tr._average_grads()
+    avg = torch.cat([p.grad.reshape(-1) for p in list(tr.actor.parameters()) + list(tr.critic.parameters())])
+    try:
+        tr._join_ranks(64 + rank)  # unequal arena counts are refused on every rank
+        refused = False
+    except ValueError:
+        refused = True
+    res = {"x": x, "st": st, "t_in": mine, "t": t, "w": w, "g_in": torch.cat(grads), "g": avg}
+    res = {k: v.detach().numpy().copy() for k, v in res.items()}  # (arrays, not shared tensors, cross the queue)
+    q.put(dict(res, rank=rank, refused=refused))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_ppo_host_logic():
+    """ppo.PPOTrainer(group=...)'s collectives on two gloo ranks: the advantage statistics over
+    both ranks' (uneven) shards equal torch's mean / std of the concatenation, the gradient
+    average is the mean of the ranks' gradients with the same bits on both, the ranks start from
+    rank 0's weights, and different arena counts are refused."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        r = q.get(timeout=120)
+        got[r["rank"]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = {r: {k: torch.from_numpy(v) if isinstance(v, np.ndarray) else v for k, v in d.items()} for r, d in got.items()}
+    allx = torch.cat([got[0]["x"], got[1]["x"]])
+    want = torch.stack([allx.double().mean(), allx.double().std()]).float()
+    for r in (0, 1):
+        assert torch.allclose(got[r]["st"], want, rtol=1e-6, atol=0), (got[r]["st"], want)
+        assert torch.allclose(got[r]["t"], (got[0]["t_in"] + got[1]["t_in"]) / 2, rtol=1e-6, atol=1e-7)
+        assert torch.allclose(got[r]["g"], (got[0]["g_in"] + got[1]["g_in"]) / 2, rtol=1e-6, atol=1e-7)
+        assert got[r]["refused"]
+    assert got[0]["t"].numpy().tobytes() == got[1]["t"].numpy().tobytes()
+    assert got[0]["g"].numpy().tobytes() == got[1]["g"].numpy().tobytes()
+    assert got[0]["w"].numpy().tobytes() == got[1]["w"].numpy().tobytes()
+    from footsies_gym_amd.rollout import make_actor
+    from footsies_gym_amd.ppo import make_critic
+    w0 = torch.cat([p.detach().reshape(-1) for n in (make_actor(seed=10), make_critic(seed=20)) for p in n.parameters()])
+    assert got[1]["w"].numpy().tobytes() == w0.numpy().tobytes()  # rank 0's initial weights
