@@ -298,6 +298,12 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 
     // ---- layer 1 on MFMA: H1^T[j][s] = b1[j] + sum_f W1[j][f] X[s][f]; K = 8 as 4 steps of
     // (f = t, t + 4): lane (r, hf) supplies A = W1[32 jb + r][t + 4 hf], B = X[r][t + 4 hf] ----
+    // (split: the tanh'd accumulators are also layer 2's B operand, straight from registers: k step
+    // 2 jb + u takes registers 8 u .. 8 u + 7 of block jb, units 32 jb + 16 u + 8 (j >> 2) + 4 hf +
+    // (j & 3) -- the k order k_ppo_frag gives W2's fragments -- so layer 2 does not wait for h1's
+    // trip through LDS; the stage is still written for the backward pass, not for the forward
+    // pass alone)
+    BF8 bh[4], bl[4];
     {
       const float4 xb = *reinterpret_cast<const float4*>(&sX[r][4 * hf]);
 #pragma unroll
@@ -308,22 +314,26 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         acc = mfma32(wa.y, xb.y, acc);
         acc = mfma32(wa.z, xb.z, acc);
         acc = mfma32(wa.w, xb.w, acc);
-        store_rows_tanh<SPLIT>(&sH1[r][32 * jb], acc, hf);
+        if constexpr (SPLIT) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q] = tanh_of<SPLIT>(acc[q]);
+          if constexpr (!EVAL) store_rows(&sH1[r][32 * jb], acc, hf);  // (the forward pass alone needs no h1 stage)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const float v[8] = {acc[8 * u], acc[8 * u + 1], acc[8 * u + 2], acc[8 * u + 3],
+                                acc[8 * u + 4], acc[8 * u + 5], acc[8 * u + 6], acc[8 * u + 7]};
+            split8(v, bh[2 * jb + u], bl[2 * jb + u]);
+          }
+        } else {
+          store_rows_tanh<SPLIT>(&sH1[r][32 * jb], acc, hf);
+        }
       }
     }
-    __syncthreads();
+    if constexpr (!SPLIT) __syncthreads();
 
     // ---- layer 2 on MFMA: H2^T[j][s] = b2[j] + sum_k W2[j][k] H1[s][k]; K = 64 as 32 steps of
     // (k = t, t + 32): A = W2[32 jb + r][t + 32 hf] (row loads), B = H1[r][t + 32 hf] (LDS row) ----
-    if constexpr (SPLIT) {  // K = 64 as 4 bf16 steps: B = H1[r][16 s + 8 hf + j], split per step
-      BF8 bh[4], bl[4];
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const float4 v0 = *reinterpret_cast<const float4*>(&sH1[r][16 * st + 8 * hf]);
-        const float4 v1 = *reinterpret_cast<const float4*>(&sH1[r][16 * st + 8 * hf + 4]);
-        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        split8(v, bh[st], bl[st]);
-      }
+    if constexpr (SPLIT) {  // K = 64 as 4 bf16 steps, B from layer 1's registers (above)
 #pragma unroll 1
       for (int jb = 0; jb < 2; ++jb) {  // (one block's fragments live at a time)
         F16 acc = bias_frag(b2v + 32 * jb, hf);
@@ -681,7 +691,10 @@ __global__ __launch_bounds__(256) void k_ppo_frag(const float* __restrict__ wa, 
   float v[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int row = 32 * blk + r, k = 16 * s + 8 * h + j;
+    // mat 0 pairs with layer 1's accumulator as the B operand, whose element j of lane half h in
+    // k step s is unit 16 s + 8 (j >> 2) + 4 h + (j & 3) (the 32 x 32 result map); mat 1 with G2
+    // rows read in natural order, k = 16 s + 8 h + j
+    const int row = 32 * blk + r, k = mat == 0 ? 16 * s + 8 * (j >> 2) + 4 * h + (j & 3) : 16 * s + 8 * h + j;
     v[j] = mat == 0 ? w[row * kH + k] : w[k * kH + row];
   }
   BF8 hi, lo;
