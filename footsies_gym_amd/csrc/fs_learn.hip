@@ -100,6 +100,14 @@ __device__ __forceinline__ F16 mfma_split(BF8 ah, BF8 al, BF8 bh, BF8 bl, F16 c)
   c = mfma_bf16(al, bh, c);
   return mfma_bf16(ah, bh, c);
 }
+// The same on v_mfma_f32_16x16x32_bf16 (K = 32 in one step): lane l holds A[row l & 15][k = 8 (l >> 4)
+// + j] and B[k = 8 (l >> 4) + j][col l & 15] in element j; the 16 x 16 accumulator D[row 4 (l >> 4) +
+// i][col l & 15] in its element i.
+__device__ __forceinline__ F4 mfma16_split(BF8 ah, BF8 al, BF8 bh, BF8 bl, F4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
 // The weight fragments of the two 64-wide GEMMs with W2 as the A operand, built once per call by
 // k_ppo_frag: [mat: 0 = W2, 1 = W2^T][row block][k step][0 = hi, 1 = lo][lane] of 8 bf16 (16 B).
 constexpr int kFragsPerNet = 2 * 2 * 4 * 2 * 64;
@@ -245,6 +253,13 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
   F16 dW2[2][2];  // dW2 as four 32 x 32 MFMA accumulators [i block][k block]
   float dW1[kF], dW3[OUT], dB3[OUT], dB2[2] = {0.f, 0.f};
   float dB1 = 0.f, pg_sum = 0.f, vf_sum = 0.f, ent_sum = 0.f;
+  // (split: dW3 and dW1 on 16 x 16 x 32 MFMAs into one set of accumulators, block b = units 16 b ..
+  // 16 b + 15 on the rows: columns 0-7 dW3[o][unit] (o < OUT), columns 8-15 dW1[unit][f]; db1 as
+  // per-lane partial sums over its 8 samples of each block, added across the lanes at the end)
+  F4 dWo[4];
+  float dB1p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < 4; ++b) dWo[b] = F4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int q = 0; q < 16; ++q) dW2[0][0][q] = dW2[0][1][q] = dW2[1][0][q] = dW2[1][1][q] = 0.f;
 #pragma unroll
@@ -474,11 +489,33 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     }
     __syncthreads();
 
-    // ---- (lane = unit j) dW3's column j from h2's column and g3's rows -------------------------
-    for (int t = 0; t < ns; ++t) {
-      const float h2c = H2[t][lane];
+    // ---- dW3 (split: D[unit][o] += sum_s H2[s][unit] G3[s][o] on 16 x 16 x 32 MFMAs, A = h2's
+    // columns, B = g3's rows in columns 0-7; padding samples have g3 = 0; fp32: lane = unit j, dW3's
+    // column j from h2's column and g3's rows) ---------------------------------------------------
+    if constexpr (SPLIT) {
+      const int c16 = lane & 15, g4 = lane >> 4;
+      BF8 bh, bl;
+      {
+        float v[8];
 #pragma unroll
-      for (int o = 0; o < OUT; ++o) dW3[o] = fmaf(sG3[t][o], h2c, dW3[o]);
+        for (int j = 0; j < 8; ++j) v[j] = c16 < 8 ? sG3[8 * g4 + j][c16 & 7] : 0.f;
+        split8(v, bh, bl);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = H2[8 * g4 + j][16 * b + c16];
+        BF8 ah, al;
+        split8(v, ah, al);
+        dWo[b] = mfma16_split(ah, al, bh, bl, dWo[b]);
+      }
+    } else {
+      for (int t = 0; t < ns; ++t) {
+        const float h2c = H2[t][lane];
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) dW3[o] = fmaf(sG3[t][o], h2c, dW3[o]);
+      }
     }
     __syncthreads();
     if constexpr (OUT == 8) {
@@ -624,8 +661,33 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     }
     __syncthreads();
 
-    // ---- (lane = unit i) dW1's row i and db1 from g1's column and x's rows ---------------------
-    for (int t = 0; t < ns; ++t) {
+    // ---- dW1 and db1 (split: D[unit][8 + f] += sum_s G1[s][unit] X[s][f] on the same accumulators,
+    // A = g1's columns, B = x's rows in columns 8-15; db1 from the A values; fp32: lane = unit i, dW1's
+    // row i and db1 from g1's column and x's rows) -----------------------------------------------
+    if constexpr (SPLIT) {
+      const int c16 = lane & 15, g4 = lane >> 4;
+      BF8 bh, bl;
+      {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = c16 >= 8 ? sX[8 * g4 + j][c16 & 7] : 0.f;
+        split8(v, bh, bl);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = sH1[8 * g4 + j][16 * b + c16];
+        float s8 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s8 += v[j];
+        dB1p[b] += s8;
+        BF8 ah, al;
+        split8(v, ah, al);
+        dWo[b] = mfma16_split(ah, al, bh, bl, dWo[b]);
+      }
+    }
+    if constexpr (!SPLIT) for (int t = 0; t < ns; ++t) {
       const float g = sH1[t][lane];
       dB1 += g;
       const float4 xa = *reinterpret_cast<const float4*>(&sX[t][0]);
@@ -645,9 +707,26 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
   if constexpr (EVAL) return;
   // ---- this wave's partial gradient --------------------------------------------------------
   float* out = partial + (size_t)blockIdx.x * partial_stride<OUT>();
+  if constexpr (SPLIT) {
+    const int c16 = lane & 15, g4 = lane >> 4;
 #pragma unroll
-  for (int f = 0; f < kF; ++f) out[lane * kF + f] = dW1[f];
-  out[kOffB1 + lane] = dB1;
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int unit = 16 * b + 4 * g4 + i;
+        if (c16 >= 8) out[unit * kF + (c16 - 8)] = dWo[b][i];
+        else if (c16 < OUT) out[kOffW3 + c16 * kH + unit] = dWo[b][i];
+      }
+      // db1 of unit 16 b + c16: the four sample groups' partial sums (lanes c16, c16 + 16, + 32, + 48)
+      float d = dB1p[b] + __shfl_xor(dB1p[b], 16, 64);
+      d += __shfl_xor(d, 32, 64);
+      if (g4 == 0) out[kOffB1 + 16 * b + c16] = d;
+    }
+  } else {
+#pragma unroll
+    for (int f = 0; f < kF; ++f) out[lane * kF + f] = dW1[f];
+    out[kOffB1 + lane] = dB1;
+  }
 #pragma unroll
   for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
@@ -662,8 +741,10 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     const float d = dB2[ib] + __shfl_xor(dB2[ib], 32, 64);  // the two sample halves
     if (hf == 0) out[kOffB2 + 32 * ib + r] = d;
   }
+  if constexpr (!SPLIT) {
 #pragma unroll
-  for (int o = 0; o < OUT; ++o) out[kOffW3 + o * kH + lane] = dW3[o];
+    for (int o = 0; o < OUT; ++o) out[kOffW3 + o * kH + lane] = dW3[o];
+  }
 #pragma unroll
   for (int o = 0; o < OUT; ++o) dB3[o] = wave_sum(dB3[o]);
   pg_sum = wave_sum(pg_sum);

@@ -61,8 +61,9 @@ def main(n=2_097_152, reps=10, only=None):
     # 2 x (forward 5 120 + backward 4 608 + weight gradients 5 120) fp32 FMAs per row, roughly
     if "hip_ms" in out:
         out["hip_tflops"] = 2 * n * 2 * (5120 + 4608 + 5120) / (out["hip_ms"] * 1e-3) / 1e12
-    if "hip_split_ms" in out:
+    if "hip_split_ms" in out and "hip_ms" in out:
         out["hip_split_speedup"] = out["hip_ms"] / out["hip_split_ms"]
+    if "eval_split_ms" in out and "eval_fp32_ms" in out:
         out["eval_split_speedup"] = out["eval_fp32_ms"] / out["eval_split_ms"]
     print(json.dumps(out))
 
