@@ -111,6 +111,7 @@ __device__ __forceinline__ F4 mfma16_split(BF8 ah, BF8 al, BF8 bh, BF8 bl, F4 c)
 // The weight fragments of the two 64-wide GEMMs with W2 as the A operand, built once per call by
 // k_ppo_frag: [mat: 0 = W2, 1 = W2^T][row block][k step][0 = hi, 1 = lo][lane] of 8 bf16 (16 B).
 constexpr int kFragsPerNet = 2 * 2 * 4 * 2 * 64;
+constexpr int kScaledPerNet = kH * kF + 2 * kH;  // 2 log2 e x (W1, b1, b2) for the split kernels
 __device__ __forceinline__ int frag_at(int mat, int blk, int s, int part, int lane) {
   return (((mat * 2 + blk) * 4 + s) * 2 + part) * 64 + lane;
 }
@@ -143,6 +144,19 @@ template <bool HW>
 __device__ __forceinline__ float tanh_of(float x) {
   if constexpr (HW) return tanh_hw(x);
   else return tanh_fast(x);
+}
+// The split-bf16 kernels' hidden layers run on weights and biases pre-scaled by 2 log2 e (W1, b1,
+// b2 and W2's layer-2 fragments, written once per call by k_ppo_frag): their pre-activations y are
+// already tanh_hw's exp2 argument, so each tanh is exp2, add, reciprocal and fma, one multiply
+// fewer (64 per lane and tile).
+constexpr float kTanhScale = 2.8853900817779268f;  // 2 log2 e
+__device__ __forceinline__ float tanh_prescaled(float y) {
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(y) + 1.f), 1.f);
+}
+template <bool HW>
+__device__ __forceinline__ float tanh_layer(float v) {  // a hidden layer's tanh (HW: of a pre-scaled value)
+  if constexpr (HW) return tanh_prescaled(v);
+  else return tanh_fast(v);
 }
 template <bool HW>
 __device__ __forceinline__ float exp_of(float x) {
@@ -214,8 +228,8 @@ template <bool HW>
 __device__ __forceinline__ void store_rows_tanh(float* dst, const F16& v, int hf) {
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq)
-    *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) = make_float4(tanh_of<HW>(v[4 * qq]), tanh_of<HW>(v[4 * qq + 1]),
-                                                                    tanh_of<HW>(v[4 * qq + 2]), tanh_of<HW>(v[4 * qq + 3]));
+    *reinterpret_cast<float4*>(dst + 8 * qq + 4 * hf) = make_float4(tanh_layer<HW>(v[4 * qq]), tanh_layer<HW>(v[4 * qq + 1]),
+                                                                    tanh_layer<HW>(v[4 * qq + 2]), tanh_layer<HW>(v[4 * qq + 3]));
 }
 
 #ifndef FSL_WAVES
@@ -331,7 +345,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         acc = mfma32(wa.w, xb.w, acc);
         if constexpr (SPLIT) {
 #pragma unroll
-          for (int q = 0; q < 16; ++q) acc[q] = tanh_of<SPLIT>(acc[q]);
+          for (int q = 0; q < 16; ++q) acc[q] = tanh_layer<SPLIT>(acc[q]);
           if constexpr (!EVAL) store_rows(&sH1[r][32 * jb], acc, hf);  // (the forward pass alone needs no h1 stage)
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
@@ -763,8 +777,18 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 // + 8 h + j]; for mat 1, W2^T[32 blk + r][...] = W2[16 s + 8 h + j][32 blk + r]; hi = bf16(w),
 // lo = bf16(w - hi).  One thread per (net, mat, blk, s, lane).
 __global__ __launch_bounds__(256) void k_ppo_frag(const float* __restrict__ wa, const float* __restrict__ wc,
-                                                 uint4* __restrict__ out) {
+                                                 uint4* __restrict__ out, const float* __restrict__ a_w1,
+                                                 const float* __restrict__ a_b1, const float* __restrict__ a_b2,
+                                                 const float* __restrict__ c_w1, const float* __restrict__ c_b1,
+                                                 const float* __restrict__ c_b2, float* __restrict__ scaled) {
   const int t = blockIdx.x * 256 + threadIdx.x;  // < 2 nets x 2 mats x 2 blks x 4 steps x 64 lanes
+  if (t < 2 * kScaledPerNet) {  // [net][W1 | b1 | b2] x 2 log2 e (tanh_prescaled); a net passed as null is skipped
+    const int net = t / kScaledPerNet, e = t - net * kScaledPerNet;
+    const float* w1 = net ? c_w1 : a_w1;
+    const float* b1 = net ? c_b1 : a_b1;
+    const float* b2 = net ? c_b2 : a_b2;
+    if (w1) scaled[t] = kTanhScale * (e < kH * kF ? w1[e] : (e < kH * kF + kH ? b1[e - kH * kF] : b2[e - kH * kF - kH]));
+  }
   if (t >= 2 * 2 * 2 * 4 * 64) return;
   const int lane = t & 63, s = (t >> 6) & 3, blk = (t >> 8) & 1, mat = (t >> 9) & 1, net = t >> 10;
   const float* w = net ? wc : wa;
@@ -773,10 +797,10 @@ __global__ __launch_bounds__(256) void k_ppo_frag(const float* __restrict__ wa, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     // mat 0 pairs with layer 1's accumulator as the B operand, whose element j of lane half h in
-    // k step s is unit 16 s + 8 (j >> 2) + 4 h + (j & 3) (the 32 x 32 result map); mat 1 with G2
-    // rows read in natural order, k = 16 s + 8 h + j
+    // k step s is unit 16 s + 8 (j >> 2) + 4 h + (j & 3) (the 32 x 32 result map), and carries
+    // tanh_prescaled's 2 log2 e; mat 1 with G2 rows read in natural order, k = 16 s + 8 h + j
     const int row = 32 * blk + r, k = mat == 0 ? 16 * s + 8 * (j >> 2) + 4 * h + (j & 3) : 16 * s + 8 * h + j;
-    v[j] = mat == 0 ? w[row * kH + k] : w[k * kH + row];
+    v[j] = mat == 0 ? kTanhScale * w[row * kH + k] : w[k * kH + row];
   }
   BF8 hi, lo;
   split8(v, hi, lo);
@@ -912,7 +936,8 @@ static size_t ppo_frag_offset() {
   return sizeof(float) * ((size_t)fsl::kMaxWaves * (fsl::partial_stride<8>() + fsl::partial_stride<1>()) +
                           2 * fsl::kH * fsl::kH);
 }
-size_t ppo_workspace_bytes() { return ppo_frag_offset() + sizeof(uint4) * 2 * fsl::kFragsPerNet; }
+static size_t ppo_scaled_offset() { return ppo_frag_offset() + sizeof(uint4) * 2 * fsl::kFragsPerNet; }
+size_t ppo_workspace_bytes() { return ppo_scaled_offset() + sizeof(float) * 2 * fsl::kScaledPerNet; }
 
 hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const actor[6], const float* const critic[6],
                            float clip, float vf_coef, float ent_coef, float* grad, float* loss, void* workspace,
@@ -927,13 +952,17 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
   uint4* frags = reinterpret_cast<uint4*>(static_cast<char*>(workspace) + ppo_frag_offset());
   hipError_t e = hipMemsetAsync(loss, 0, 3 * sizeof(float), s);
   if (e != hipSuccess) return e;
-  if (split) {
-    hipLaunchKernelGGL(k_ppo_frag, dim3(8), dim3(256), 0, s, actor[2], critic[2], frags);
-    hipLaunchKernelGGL((k_ppo_grad<8, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1],
-                       actor[2], actor[3], actor[4], actor[5], c, pa, nullptr, nullptr, frags, runs, run_shift, n_rows);
-    hipLaunchKernelGGL((k_ppo_grad<1, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1],
-                       critic[2], critic[3], critic[4], critic[5], c, pc, nullptr, nullptr, frags + kFragsPerNet, runs, run_shift,
+  if (split) {  // (W1, b1, b2 as 2 log2 e x their values from the workspace: tanh_prescaled)
+    float* sc = reinterpret_cast<float*>(static_cast<char*>(workspace) + ppo_scaled_offset());
+    float *sa = sc, *sk = sc + kScaledPerNet;
+    hipLaunchKernelGGL(k_ppo_frag, dim3(8), dim3(256), 0, s, actor[2], critic[2], frags, actor[0], actor[1], actor[3],
+                       critic[0], critic[1], critic[3], sc);
+    hipLaunchKernelGGL((k_ppo_grad<8, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, sa, sa + kH * kF,
+                       actor[2], sa + kH * kF + kH, actor[4], actor[5], c, pa, nullptr, nullptr, frags, runs, run_shift,
                        n_rows);
+    hipLaunchKernelGGL((k_ppo_grad<1, false, true>), dim3(waves), dim3(64), 0, s, rows, n, tiles, sk, sk + kH * kF,
+                       critic[2], sk + kH * kF + kH, critic[4], critic[5], c, pc, nullptr, nullptr, frags + kFragsPerNet,
+                       runs, run_shift, n_rows);
   } else {
     hipLaunchKernelGGL(k_ppo_t64, dim3(4, 2), dim3(256), 0, s, actor[2], critic[2], w2t);
     hipLaunchKernelGGL(k_ppo_grad<8>, dim3(waves), dim3(64), 0, s, rows, n, tiles, actor[0], actor[1], actor[2],
@@ -954,19 +983,26 @@ hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* acti
   using namespace fsl;
   const Coef c{0.f, 0.f, 0.f, 0.f};
   uint4* frags = split ? reinterpret_cast<uint4*>(static_cast<char*>(workspace) + ppo_frag_offset()) : nullptr;
+  float* sc = split ? reinterpret_cast<float*>(static_cast<char*>(workspace) + ppo_scaled_offset()) : nullptr;
   const bool run_v = values && n_values > 0, run_l = logp && n_logp > 0;
   if (split) {  // (a network not run passes its actor / critic arrays as null: its fragments are not built)
     const float* wa = run_l ? actor[2] : (run_v ? critic[2] : nullptr);
     const float* wc = run_v ? critic[2] : wa;
-    if (wa) hipLaunchKernelGGL(k_ppo_frag, dim3(8), dim3(256), 0, s, wa, wc, frags);
+    const float* const* na = run_l ? actor : nullptr;
+    const float* const* nc = run_v ? critic : nullptr;
+    if (wa)
+      hipLaunchKernelGGL(k_ppo_frag, dim3(8), dim3(256), 0, s, wa, wc, frags, na ? na[0] : nullptr, na ? na[1] : nullptr,
+                         na ? na[3] : nullptr, nc ? nc[0] : nullptr, nc ? nc[1] : nullptr, nc ? nc[3] : nullptr, sc);
   }
   if (run_v) {
     const int64_t tiles = (n_values + kTile - 1) / kTile;
     const int waves = (int)(tiles < kMaxEvalWaves ? tiles : kMaxEvalWaves);
-    if (split)
-      hipLaunchKernelGGL((k_ppo_grad<1, true, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, critic[0],
-                         critic[1], critic[2], critic[3], critic[4], critic[5], c, values, nullptr, nullptr,
+    if (split) {
+      const float* sk = sc + kScaledPerNet;
+      hipLaunchKernelGGL((k_ppo_grad<1, true, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, sk, sk + kH * kF,
+                         critic[2], sk + kH * kF + kH, critic[4], critic[5], c, values, nullptr, nullptr,
                          frags + kFragsPerNet);
+    }
     else
       hipLaunchKernelGGL((k_ppo_grad<1, true>), dim3(waves), dim3(64), 0, s, x, n_values, tiles, critic[0], critic[1],
                          critic[2], critic[3], critic[4], critic[5], c, values, nullptr);
@@ -975,8 +1011,8 @@ hipError_t launch_ppo_eval(const float* x, int64_t n_values, const uint8_t* acti
     const int64_t tiles = (n_logp + kTile - 1) / kTile;
     const int waves = (int)(tiles < kMaxEvalWaves ? tiles : kMaxEvalWaves);
     if (split)
-      hipLaunchKernelGGL((k_ppo_grad<8, true, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, actor[0],
-                         actor[1], actor[2], actor[3], actor[4], actor[5], c, logp, actions, nullptr, frags);
+      hipLaunchKernelGGL((k_ppo_grad<8, true, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, sc, sc + kH * kF,
+                         actor[2], sc + kH * kF + kH, actor[4], actor[5], c, logp, actions, nullptr, frags);
     else
       hipLaunchKernelGGL((k_ppo_grad<8, true>), dim3(waves), dim3(64), 0, s, x, n_logp, tiles, actor[0], actor[1],
                          actor[2], actor[3], actor[4], actor[5], c, logp, actions);
