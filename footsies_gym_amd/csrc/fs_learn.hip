@@ -78,8 +78,8 @@ typedef __bf16 BF8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ F16 mfma_bf16(BF8 a, BF8 b, F16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-// (as pairs: one v_cvt_pk_bf16_f32 rounds two values, one v_pk_add_f32 forms two remainders; the
-// library is built without SLP vectorization, so the pairs are spelled out)
+// (as pairs: one v_cvt_pk_bf16_f32 rounds two values and one the two remainders; the library is
+// built without SLP vectorization, so the pairs are spelled out)
 typedef float F2 __attribute__((ext_vector_type(2)));
 typedef __bf16 BF2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split8(const float (&x)[8], BF8& hi, BF8& lo) {
@@ -87,7 +87,11 @@ __device__ __forceinline__ void split8(const float (&x)[8], BF8& hi, BF8& lo) {
   for (int j = 0; j < 8; j += 2) {
     const F2 v = {x[j], x[j + 1]};
     const BF2 h = __builtin_convertvector(v, BF2);
-    const BF2 l = __builtin_convertvector(v - __builtin_convertvector(h, F2), BF2);
+    const F2 hf = __builtin_convertvector(h, F2);
+    // the remainders as two plain subtractions: a v_pk_add_f32 wants its operands in an aligned
+    // register pair, which values read from the stages' columns are not (two moves per pair)
+    const F2 r = {__fsub_rn(x[j], hf[0]), __fsub_rn(x[j + 1], hf[1])};
+    const BF2 l = __builtin_convertvector(r, BF2);
     hi[j] = h[0];
     hi[j + 1] = h[1];
     lo[j] = l[0];
