@@ -47,6 +47,17 @@ template <int OUT>
 constexpr int off_b3() { return kOffW3 + OUT * kH; }
 
 using CPtr = const __attribute__((address_space(4))) float*;  // scalar (constant) loads
+// Weight pointers made opaque per tile (below) lose their address space; as generic pointers their
+// loads become flat loads with a 64-bit address add each (flat loads also wait on both counters).
+// Cast back to global memory they load with an SGPR base and a 32-bit lane offset.
+using GPtr = const __attribute__((address_space(1))) float*;
+typedef float F4v __attribute__((ext_vector_type(4)));  // (a native vector: copies from any address space)
+using GPtr4 = const __attribute__((address_space(1))) F4v*;
+// (an unsigned 32-bit element index: the load can take it as its VGPR offset beside the SGPR base)
+__device__ __forceinline__ float4 ld4(GPtr p, uint32_t i) {
+  const F4v v = *(GPtr4)(p + i);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
 
 struct Coef {
   float clip, vf_coef, ent_coef, inv_n;
@@ -116,8 +127,14 @@ __device__ __forceinline__ F4 mfma16_split(BF8 ah, BF8 al, BF8 bh, BF8 bl, F4 c)
 // k_ppo_frag: [mat: 0 = W2, 1 = W2^T][row block][k step][0 = hi, 1 = lo][lane] of 8 bf16 (16 B).
 constexpr int kFragsPerNet = 2 * 2 * 4 * 2 * 64;
 constexpr int kScaledPerNet = kH * kF + 2 * kH;  // 2 log2 e x (W1, b1, b2) for the split kernels
-__device__ __forceinline__ int frag_at(int mat, int blk, int s, int part, int lane) {
-  return (((mat * 2 + blk) * 4 + s) * 2 + part) * 64 + lane;
+__device__ __forceinline__ uint32_t frag_at(int mat, int blk, int s, int part, int lane) {  // (unsigned: see ld4)
+  return (uint32_t)((((mat * 2 + blk) * 4 + s) * 2 + part) * 64 + lane);
+}
+// one fragment, loaded through a global-memory pointer
+__device__ __forceinline__ BF8 ldfrag(const uint4* frags, uint32_t i) {
+  typedef uint32_t U4v __attribute__((ext_vector_type(4)));
+  using G4 = const __attribute__((address_space(1))) U4v*;
+  return __builtin_bit_cast(BF8, ((G4)frags)[i]);
 }
 
 // tanh without branches (the library tanhf runs both of its branches under divergence, ~30
@@ -214,11 +231,11 @@ __device__ __forceinline__ void actor_loss(const float (&z)[8], const float (&ta
 // Accumulator element q of lane (r, hf) is row (q & 3) + 8 (q >> 2) + 4 hf, column r: four runs
 // of four consecutive rows.  bias_frag: the accumulator holding b[row] in every column;
 // store_rows(_tanh): (tanh of) column r's 16 values into the LDS row `dst` (= stage[r] + 32 block).
-__device__ __forceinline__ F16 bias_frag(const float* b, int hf) {
+__device__ __forceinline__ F16 bias_frag(GPtr b, int hf) {
   F16 v;
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) {
-    const float4 x = *reinterpret_cast<const float4*>(b + 8 * qq + 4 * hf);
+    const float4 x = ld4(b, (uint32_t)(8 * qq + 4 * hf));
     v[4 * qq] = x.x; v[4 * qq + 1] = x.y; v[4 * qq + 2] = x.z; v[4 * qq + 3] = x.w;
   }
   return v;
@@ -300,6 +317,8 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     const float *w1v = w1, *b1v = b1, *w2v = w2, *b2v = b2, *w3v = w3, *b3v = b3, *w2tv = w2t;
     asm volatile("" : "+s"(w1v), "+s"(b1v), "+s"(w2v), "+s"(b2v), "+s"(w3v), "+s"(b3v), "+s"(w2tv));
     const CPtr W3 = (CPtr)w3v, B3 = (CPtr)b3v;
+    const GPtr w1g = (GPtr)w1v, b1g = (GPtr)b1v, w2g = (GPtr)w2v, b2g = (GPtr)b2v, w3g = (GPtr)w3v, b3g = (GPtr)b3v,
+               w2tg = (GPtr)w2tv;
     const int64_t left = n - tile * kTile;
     const int ns = (int)(left < kTile ? left : kTile);
     int64_t row = tile * kTile + lane;
@@ -341,8 +360,8 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       const float4 xb = *reinterpret_cast<const float4*>(&sX[r][4 * hf]);
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
-        const float4 wa = *reinterpret_cast<const float4*>(&w1v[(32 * jb + r) * kF + 4 * hf]);
-        F16 acc = bias_frag(b1v + 32 * jb, hf);
+        const float4 wa = ld4(w1g, (uint32_t)((32 * jb + r) * kF + 4 * hf));
+        F16 acc = bias_frag(b1g + 32 * jb, hf);
         acc = mfma32(wa.x, xb.x, acc);
         acc = mfma32(wa.y, xb.y, acc);
         acc = mfma32(wa.z, xb.z, acc);
@@ -369,11 +388,11 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
     if constexpr (SPLIT) {  // K = 64 as 4 bf16 steps, B from layer 1's registers (above)
 #pragma unroll 1
       for (int jb = 0; jb < 2; ++jb) {  // (one block's fragments live at a time)
-        F16 acc = bias_frag(b2v + 32 * jb, hf);
+        F16 acc = bias_frag(b2g + 32 * jb, hf);
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
-          const BF8 ah = __builtin_bit_cast(BF8, frags[frag_at(0, jb, st, 0, lane)]);
-          const BF8 al = __builtin_bit_cast(BF8, frags[frag_at(0, jb, st, 1, lane)]);
+          const BF8 ah = ldfrag(frags, frag_at(0, jb, st, 0, lane));
+          const BF8 al = ldfrag(frags, frag_at(0, jb, st, 1, lane));
           acc = mfma_split(ah, al, bh[st], bl[st], acc);
         }
         store_rows_tanh<SPLIT>(&H2[r][32 * jb], acc, hf);
@@ -390,10 +409,10 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         float wa[32];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const float4 v = *reinterpret_cast<const float4*>(&w2v[(32 * jb + r) * kH + 32 * hf + 4 * u]);
+          const float4 v = ld4(w2g, (uint32_t)((32 * jb + r) * kH + 32 * hf + 4 * u));
           wa[4 * u] = v.x; wa[4 * u + 1] = v.y; wa[4 * u + 2] = v.z; wa[4 * u + 3] = v.w;
         }
-        F16 acc = bias_frag(b2v + 32 * jb, hf);
+        F16 acc = bias_frag(b2g + 32 * jb, hf);
 #pragma unroll
         for (int t = 0; t < 32; ++t) acc = mfma32(wa[t], hb[t], acc);
         store_rows_tanh<SPLIT>(&H2[r][32 * jb], acc, hf);
@@ -451,11 +470,11 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
       float wz[16];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float4 v = c16 < 8 ? *reinterpret_cast<const float4*>(&w3v[c16 * kH + 16 * q4 + 4 * u])
+        const float4 v = c16 < 8 ? ld4(w3g, (uint32_t)(c16 * kH + 16 * q4 + 4 * u))
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         wz[4 * u] = v.x; wz[4 * u + 1] = v.y; wz[4 * u + 2] = v.z; wz[4 * u + 3] = v.w;
       }
-      const float4 bz = q4 < 2 ? *reinterpret_cast<const float4*>(&b3v[4 * q4]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 bz = q4 < 2 ? ld4(b3g, (uint32_t)(4 * q4)) : make_float4(0.f, 0.f, 0.f, 0.f);
       F4 zacc[2];
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
@@ -548,7 +567,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc = mfma32(w3v[(t + 4 * hf) * kH + 32 * jb + r], gb[t], acc);
+        for (int t = 0; t < 4; ++t) acc = mfma32(w3g[(uint32_t)((t + 4 * hf) * kH + 32 * jb + r)], gb[t], acc);
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           float4* hp = reinterpret_cast<float4*>(&H2[r][32 * jb + 8 * qq + 4 * hf]);
@@ -566,7 +585,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const int j = 32 * jb + 8 * qq + 4 * hf;
-          const float4 w = *reinterpret_cast<const float4*>(&w3v[j]);
+          const float4 w = ld4(w3g, (uint32_t)j);
           float4* hp = reinterpret_cast<float4*>(&H2[r][j]);
           const float4 hv = *hp;
           *hp = make_float4(fmaf(w.x, g3, 0.f) * (1.f - hv.x * hv.x), fmaf(w.y, g3, 0.f) * (1.f - hv.y * hv.y),
@@ -636,8 +655,8 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
-          const BF8 ah = __builtin_bit_cast(BF8, frags[frag_at(1, ib, st, 0, lane)]);
-          const BF8 al = __builtin_bit_cast(BF8, frags[frag_at(1, ib, st, 1, lane)]);
+          const BF8 ah = ldfrag(frags, frag_at(1, ib, st, 0, lane));
+          const BF8 al = ldfrag(frags, frag_at(1, ib, st, 1, lane));
           acc = mfma_split(ah, al, gh[st], gl[st], acc);
         }
 #pragma unroll
@@ -660,7 +679,7 @@ __global__ __launch_bounds__(64) FSL_OCC void k_ppo_grad(const float* __restrict
         float wa[32];  // W2's column 32 ib + r = row 32 ib + r of W2^T (k_ppo_t64), as float4s
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const float4 v = *reinterpret_cast<const float4*>(&w2tv[(32 * ib + r) * kH + 32 * hf + 4 * u]);
+          const float4 v = ld4(w2tg, (uint32_t)((32 * ib + r) * kH + 32 * hf + 4 * u));
           wa[4 * u] = v.x; wa[4 * u + 1] = v.y; wa[4 * u + 2] = v.z; wa[4 * u + 3] = v.w;
         }
         F16 acc;
