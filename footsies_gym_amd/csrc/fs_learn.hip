@@ -39,7 +39,7 @@ constexpr int kMaxEvalWaves = 4096;  // the forward pass alone: four (fewer regi
 template <int OUT>
 constexpr int n_params() { return kH * kF + kH + kH * kH + kH + OUT * kH + OUT; }
 template <int OUT>
-constexpr int partial_stride() { return (n_params<OUT>() + 3 + 3) & ~3; }  // + pg / vf / ent sums
+constexpr int partial_stride() { return (n_params<OUT>() + 3 + 31) & ~31; }  // + pg / vf / ent sums; 128-B rows
 
 // parameter offsets in torch's parameters() order: w1, b1, w2, b2, w3, b3
 constexpr int kOffB1 = kH * kF, kOffW2 = kOffB1 + kH, kOffB2 = kOffW2 + kH * kH, kOffW3 = kOffB2 + kH;
@@ -845,30 +845,41 @@ __global__ __launch_bounds__(256) void k_ppo_t64(const float* __restrict__ wa, c
   }
 }
 
-// Sum the partials of `waves` waves in a fixed order: thread (g, p) adds waves g, g + 16, ...
-// of entry p, then thread g = 0 adds the 16 sums in order.  Entries past the parameters are the
-// loss sums; they are added into loss_out scaled by 1/n.
-template <int OUT>
-__global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial, int waves,
-                                                     float* __restrict__ grad, float* __restrict__ loss, float inv_n) {
-  __shared__ float sum[16][64];
-  const int pl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int p = blockIdx.x * 64 + pl;
-  constexpr int P = n_params<OUT>(), S = partial_stride<OUT>();
+// Sum the partials of `waves` waves in a fixed order, both networks in one launch: blocks
+// [0, nba) take the actor's entries, the rest the critic's, 32 entries (one 128-B line of every
+// partial row) per block.  Thread (g, p) adds waves g, g + 32, ... of entry p, then thread g = 0
+// adds the 32 sums in order.  Entries past a network's parameters are its loss sums; each loss
+// term is written by the one network that has it (the actor's policy and entropy, the critic's
+// value; the other network's slot is 0), scaled by 1/n.  One launch of ~316 blocks keeps every
+// CU loading, where one 83-block launch per network left two thirds of them idle.
+constexpr int kRedLanes = 32, kRedGroups = 32;
+__global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ pa, const float* __restrict__ pc,
+                                                     int waves, int nba, float* __restrict__ grad,
+                                                     float* __restrict__ loss, float inv_n) {
+  __shared__ float sum[kRedGroups][kRedLanes];
+  const int pl = threadIdx.x & (kRedLanes - 1), g = threadIdx.x / kRedLanes;
+  const bool actor = (int)blockIdx.x < nba;
+  const int P = actor ? n_params<8>() : n_params<1>();
+  const size_t S = actor ? partial_stride<8>() : partial_stride<1>();
+  const float* partial = actor ? pa : pc;
+  const int p = ((int)blockIdx.x - (actor ? 0 : nba)) * kRedLanes + pl;
   float a = 0.f;
   if (p < P + 3) {
-    // unrolled so eight loads are in flight per thread; the additions keep their order
-#pragma unroll 8
-    for (int w = g; w < waves; w += 16) a += partial[(size_t)w * S + p];
+    // unrolled so sixteen loads are in flight per thread; the additions keep their order
+#pragma unroll 16
+    for (int w = g; w < waves; w += kRedGroups) a += partial[(size_t)w * S + p];
   }
   sum[g][pl] = a;
   __syncthreads();
   if (g == 0 && p < P + 3) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) t += sum[i][pl];
-    if (p < P) grad[p] = t;
-    else loss[p - P] += t * inv_n;
+    for (int i = 0; i < kRedGroups; ++i) t += sum[i][pl];
+    if (p < P) {
+      grad[(actor ? 0 : n_params<8>()) + p] = t;
+    } else if ((p - P == 1) != actor) {
+      loss[p - P] = 0.f + t * inv_n;
+    }
   }
 }
 
@@ -973,8 +984,6 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
   float* pc = pa + (size_t)kMaxWaves * partial_stride<8>();
   float* w2t = pc + (size_t)kMaxWaves * partial_stride<1>();  // [2][64][64]: actor, critic
   uint4* frags = reinterpret_cast<uint4*>(static_cast<char*>(workspace) + ppo_frag_offset());
-  hipError_t e = hipMemsetAsync(loss, 0, 3 * sizeof(float), s);
-  if (e != hipSuccess) return e;
   if (split) {  // (W1, b1, b2 as 2 log2 e x their values from the workspace: tanh_prescaled)
     float* sc = reinterpret_cast<float*>(static_cast<char*>(workspace) + ppo_scaled_offset());
     float *sa = sc, *sk = sc + kScaledPerNet;
@@ -993,10 +1002,9 @@ hipError_t launch_ppo_grad(const float* rows, int64_t n, const float* const acto
     hipLaunchKernelGGL(k_ppo_grad<1>, dim3(waves), dim3(64), 0, s, rows, n, tiles, critic[0], critic[1], critic[2],
                        critic[3], critic[4], critic[5], c, pc, nullptr, w2t + kH * kH, nullptr, runs, run_shift, n_rows);
   }
-  hipLaunchKernelGGL(k_ppo_reduce<8>, dim3((n_params<8>() + 3 + 63) / 64), dim3(1024), 0, s, pa, waves, grad, loss,
+  const int nba = (n_params<8>() + 3 + kRedLanes - 1) / kRedLanes, nbc = (n_params<1>() + 3 + kRedLanes - 1) / kRedLanes;
+  hipLaunchKernelGGL(k_ppo_reduce, dim3(nba + nbc), dim3(kRedLanes * kRedGroups), 0, s, pa, pc, waves, nba, grad, loss,
                      c.inv_n);
-  hipLaunchKernelGGL(k_ppo_reduce<1>, dim3((n_params<1>() + 3 + 63) / 64), dim3(1024), 0, s, pc, waves,
-                     grad + n_params<8>(), loss, c.inv_n);
   return hipGetLastError();
 }
 
