@@ -892,9 +892,37 @@ __global__ __launch_bounds__(256) void k_ppo_gae(const double* __restrict__ rew,
                                                  float gamma_lam, float* __restrict__ adv, float* __restrict__ ret) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
+  // ticks in batches of kU, every load of a batch issued before its recursion runs (one wave per
+  // SIMD at C5's 65 536 arenas: the loads in flight, not the arithmetic, set the pace); v[t + 1]
+  // of tick t is the batch's previous tick's v[t], so val is read once per tick.  The T mod kU
+  // ticks left at the start of the trajectory run one by one.
+  constexpr int kU = 16;
   float a = 0.f;
-#pragma unroll 4
-  for (int t = T - 1; t >= 0; --t) {
+  int t = T - 1;
+  for (; t + 1 >= kU; t -= kU) {  // ticks t, t - 1, ..., t - kU + 1
+    uint8_t d[kU];
+    float v[kU + 1];
+    double r[kU];
+    v[0] = val[(int64_t)(t + 1) * N + n];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = (int64_t)(t - u) * N + n;
+      d[u] = done[i];
+      v[u + 1] = val[i];
+      r[u] = rew[i];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink each load to its use)
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = (int64_t)(t - u) * N + n;
+      const float keep = 1.f - (float)d[u];
+      const float delta = ((float)r[u] + (gamma * v[u]) * keep) - v[u + 1];
+      a = t - u == T - 1 ? delta : fmaf(gamma_lam * keep, a, delta);
+      adv[i] = a;
+      ret[i] = a + v[u + 1];
+    }
+  }
+  for (; t >= 0; --t) {
     const int64_t i = (int64_t)t * N + n;
     const float keep = 1.f - (float)done[i];
     const float v0 = val[i];
